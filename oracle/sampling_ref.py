@@ -1,0 +1,293 @@
+"""ORACLE (test infrastructure only) -- numpy restatement of the annealed-Langevin samplers
+and the cross-view consistency merge.
+
+Follows, with the reference's dtype semantics (float32 images, float64 projection):
+  * Langevin update ...... LiDARGen/models/KITTISampling.py:133-156, models/__init__.py:1397-1416
+  * kitti merge .......... LiDARGen/models/KITTISampling.py:160-490 (pose matrices)
+  * AllForOne merge ...... LiDARGen/models/__init__.py:209-579 (origin offsets)
+  * samplers ............. KITTISampling.py:6-513, models/__init__.py:112-602, :1385-1442
+
+The reference sorts (argsort / 2 stable sorts / unique_consecutive) and sums duplicates
+through sparse->dense; this restatement computes the same per-cell quantities with
+scatter reductions (count, sum of log-depth, sum of intensity, nearest point).  Two
+documented differences, both below the stated tolerances: duplicate sums are taken in
+float64 (the reference sums intensities in float32 in depth order), and a tie between
+equal nearest depths keeps the lowest source index (the reference's argsort is unstable,
+so its choice is unspecified).  Pinned by tests/golden/merge_*.npz.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+F32 = np.float32
+
+
+# ----------------------------------------------------------------------------- geometry
+def merge_geometry(H: int, W: int) -> dict:
+    """Constants of KITTISampling.py:29-102 (identical in models/__init__.py:131-207)."""
+    hA = math.radians(360) / W
+    vA = math.radians(28) / H
+    hMin = ((W * -180) // 360) * hA + hA / 2
+    big = int((max(abs(-25), abs(3)) * 2) * H // 28)
+    bigMin = (big // -2) * vA + vA / 2
+    vMin = ((H * -25) // 28) * vA + vA / 2
+    az = np.arange(W - 1, -1, -1) * hA + hMin
+    el = np.arange(H - 1, -1, -1) * vA + vMin
+    return dict(H=H, W=W, hA=hA, vA=vA, hMin=hMin, big=big, bigMin=bigMin, az=az, el=el)
+
+
+def sigma_mod_of(sigma):
+    """KITTISampling.py:124-126: sigmaMod = sigma if sigma > 1 else 1."""
+    return F32(sigma) if sigma > 1 else F32(1.0)
+
+
+def real_distance(x0: np.ndarray, smod) -> np.ndarray:
+    """KITTISampling.py:164-166: (2^(|x|*6/smod) - 1) * (+1 | -1 for negative codes), float32."""
+    v = (np.abs(x0) * F32(6)) / F32(smod)
+    rd = np.exp2(v.astype(np.float64)).astype(F32) - F32(1)   # correctly rounded f32 2^v
+    mod = np.where(x0 < 0, F32(-1), F32(1)).astype(F32)
+    return (rd * mod).astype(F32)
+
+
+def min_depth_threshold(smod) -> np.float32:
+    """KITTISampling.py:272-274: log2(tensor(0.2)+1)/6*sigmaMod evaluated in float32."""
+    l2 = F32(np.log2(np.float64(F32(F32(0.2) + F32(1)))))   # correctly rounded f32 log2
+    return F32(F32(l2 / F32(6)) * F32(smod))
+
+
+def _bin(q, g):
+    """Project relative points q [3,N] (float64) -> (row, col, logdepth-code before *smod)."""
+    xy = q[0] * q[0] + q[1] * q[1]
+    d = np.sqrt(xy + q[2] * q[2])
+    h = np.arctan2(q[1], q[0])
+    e = np.arctan2(q[2], np.sqrt(xy))
+    col = np.rint((h - g["hMin"]) / g["hA"])
+    row = np.rint((e - g["bigMin"]) / g["vA"])
+    col = (g["W"] - 1 - col)
+    row = (g["big"] - 1 - row)
+    return row, col, d
+
+
+def _accumulate(row, col, ell, inten, valid, g):
+    """Per-cell count / sum(l) / sum(I) / nearest point of one output view."""
+    W, big = g["W"], g["big"]
+    cells = big * W
+    r = row[valid].astype(np.int64)
+    c = col[valid].astype(np.int64)
+    idx = r * W + c
+    lv = ell[valid]
+    iv = inten[valid].astype(np.float64)
+    n = np.bincount(idx, minlength=cells)
+    sl = np.bincount(idx, weights=lv, minlength=cells)
+    si = np.bincount(idx, weights=iv, minlength=cells)
+    # nearest point: smallest l, ties -> lowest source index
+    order = np.lexsort((np.arange(idx.size), lv, idx))
+    first = np.ones(order.size, bool)
+    first[1:] = idx[order][1:] != idx[order][:-1]
+    sel = order[first]
+    lmin = np.zeros(cells)
+    imin = np.zeros(cells, np.float32)
+    lmin[idx[sel]] = lv[sel]
+    imin[idx[sel]] = inten[valid][sel]
+    return n, sl, si, lmin, imin
+
+
+def _resolve(n, sl, si, lmin, imin, smod, allowance, controlled: bool):
+    """KITTISampling.py:306-326 (controlled average) / models/__init__.py:441-481."""
+    scaling = (n.astype(np.float32) + F32(1e-9)).astype(np.float32)
+    A_code = sl / scaling.astype(np.float64)
+    Ibar = (si / scaling.astype(np.float64)).astype(np.float32)
+    if not controlled:
+        return A_code, Ibar, n > 0
+    A = np.power(2.0, np.abs(A_code) * 6 / np.float64(F32(smod))) - 1
+    M = np.power(2.0, np.abs(lmin) * 6 / np.float64(F32(smod))) - 1
+    cond = A > M + allowance
+    I = np.where(cond, imin, Ibar).astype(np.float32)
+    D = np.where(cond, M + allowance / 5, A)
+    code = np.log2(D + 1) / 6 * np.float64(F32(smod))
+    return code, I, n > 0
+
+
+def _crop_flip(code, I, cm, isneg_o, g):
+    """Crop rows big-H.. and use flip(roll(., W/2)) for negative pixels (KITTISampling.py:349-358)."""
+    H, W, big = g["H"], g["W"], g["big"]
+    code = code.reshape(big, W)
+    I = I.reshape(big, W)
+    cm = cm.reshape(big, W)
+    top = slice(big - H, big)
+    fcode = np.flip(np.roll(code, W // 2, axis=1), axis=0)[top]
+    fI = np.flip(np.roll(I, W // 2, axis=1), axis=0)[top]
+    fcm = np.flip(np.roll(cm, W // 2, axis=1), axis=0)[top]
+    depth = np.where(isneg_o, -fcode, code[top])
+    inten = np.where(isneg_o, fI, I[top])
+    cmask = np.where(isneg_o, fcm, cm[top])
+    return depth, inten, cmask
+
+
+def _apply(x, new, maskimg, sky, refmask, too_high, cc):
+    """KITTISampling.py:411-490: correction on unknown pixels, zeroed when tooHigh."""
+    m = np.logical_and(maskimg[:, None], sky)  # [B,1,H,W]
+    corr = -(m.astype(np.int32) * (1 - (refmask != 0)).astype(np.int32)).astype(np.float32) * (x - new)
+    if too_high:
+        corr = np.zeros_like(corr)
+    return (x + F32(cc) * corr).astype(np.float32)
+
+
+def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5, allowance=10, cc=0.01):
+    """One consistency merge of the pose-matrix sampler (KITTISampling.py:160-490).
+
+    x f32 [B,2,H,W] (after the Langevin update); returns (newImages f32, x corrected f32).
+    """
+    B, _, H, W = x.shape
+    g = merge_geometry(H, W)
+    smod = sigma_mod_of(sigma)
+    x0 = x[:, 0]
+    isneg = x0 < 0
+    too_high = bool(F32(F32(np.abs(x0).max()) * F32(6)) / F32(smod) > 50)
+    rd = real_distance(x0, smod).astype(np.float64)
+    caz, saz = np.cos(g["az"])[None, None, :], np.sin(g["az"])[None, None, :]
+    cel, sel = np.cos(g["el"])[None, :, None], np.sin(g["el"])[None, :, None]
+    P = np.stack([(rd * caz * cel).reshape(B, -1), (rd * saz * cel).reshape(B, -1),
+                  (rd * sel).reshape(B, -1), np.ones((B, H * W))], 1)
+    Pw = np.einsum("bij,bjn->bin", toWorld, P)
+    thr = np.float64(min_depth_threshold(smod))
+    ex = exist[:aB].reshape(-1)
+    new = np.zeros_like(x)
+    maskimg = np.zeros((B, H, W), bool)
+    for o in range(B):
+        m0 = (o // aB) * aB
+        src = Pw[m0:m0 + aB]                                 # [aB,4,HW]
+        q = np.einsum("ij,vjn->vin", fromWorld[o], src)[:, :3].transpose(1, 0, 2).reshape(3, -1)
+        row, col, d = _bin(q, g)
+        ell = np.log2(d + 1) / 6 * np.float64(smod)
+        valid = (col > -1) & (col < W) & (row > -1) & (row < g["big"]) & ex
+        if setting == 5:
+            valid &= ell > thr
+        inten = x[m0:m0 + aB, 1].reshape(-1)
+        acc = _accumulate(row, col, ell, inten, valid, g)
+        code, I, cm = _resolve(*acc, smod, allowance, controlled=True)
+        dep, inn, cmask = _crop_flip(code, I, cm, isneg[o], g)
+        new[o, 0] = dep.astype(np.float32)
+        new[o, 1] = inn
+        maskimg[o] = np.logical_and(exist[0], cmask)
+    return new, _apply(x, new, maskimg, sky, refmask, too_high, cc)
+
+
+def allforone_origins(mods) -> np.ndarray:
+    """models/__init__.py:224-231 evaluated in float32: 10*sign(m) up to rounding."""
+    m = np.asarray(mods, np.int64)
+    # each transcendental in float64 then rounded: the correctly rounded float32 result
+    l2 = np.log2((np.abs(m) + 1).astype(np.float64)).astype(np.float32)
+    o = (l2 / F32(6)) * F32(1)
+    o = np.exp2((o * F32(6)).astype(np.float32).astype(np.float64)).astype(np.float32) - F32(1)
+    den = (m.astype(np.float32) + F32(1e-8)).astype(np.float32)
+    return ((o / den).astype(np.float32) * F32(10)).astype(np.float32)
+
+
+def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01):
+    """One merge of the origin-offset sampler (models/__init__.py:263-579)."""
+    B, _, H, W = x.shape
+    g = merge_geometry(H, W)
+    smod = sigma_mod_of(sigma)
+    x0 = x[:, 0]
+    isneg = x0 < 0
+    too_high = bool(F32(F32(np.abs(x0).max()) * F32(6)) / F32(smod) > 50)
+    rd = real_distance(x0, smod).astype(np.float64)
+    org = allforone_origins(mods).astype(np.float64)[:aB]       # [aB,3]
+    caz, saz = np.cos(g["az"])[None, None, :], np.sin(g["az"])[None, None, :]
+    cel, sel = np.cos(g["el"])[None, :, None], np.sin(g["el"])[None, :, None]
+    thr = np.float64(min_depth_threshold(smod))
+    ex = exist[:aB].reshape(-1)
+    allowance = 5 if setting >= 8 else 10
+    new = np.zeros_like(x)
+    maskimg = np.zeros((B, H, W), bool)
+    for o in range(B):
+        m0 = (o // aB) * aB
+        r = rd[m0:m0 + aB]
+        px = (r * caz * cel + org[:, 0, None, None]).reshape(-1)
+        py = (r * saz * cel + org[:, 1, None, None]).reshape(-1)
+        pz = (r * sel + org[:, 2, None, None]).reshape(-1)
+        oo = org[o - m0]
+        q = np.stack([px - oo[0], py - oo[1], pz - oo[2]])
+        row, col, d = _bin(q, g)
+        ell = np.log2(d + 1) / 6 * np.float64(smod)
+        valid = (col > -1) & (col < W) & (row > -1) & (row < g["big"])
+        valid &= sky[m0:m0 + aB].reshape(-1) & ex & (ell > thr)
+        inten = x[m0:m0 + aB, 1].reshape(-1)
+        acc = _accumulate(row, col, ell, inten, valid, g)
+        code, I, cm = _resolve(*acc, smod, allowance, controlled=setting >= 7)
+        dep, inn, cmask = _crop_flip(code, I, cm, isneg[o], g)
+        new[o, 0] = dep.astype(np.float32)
+        new[o, 1] = inn
+        maskimg[o] = np.logical_and(exist[0], cmask)
+    return new, _apply(x, new, maskimg, sky, refmask, too_high, cc)
+
+
+# ----------------------------------------------------------------------------- Langevin
+def nan_to_num(g):
+    """torch.nan_to_num defaults (KITTISampling.py:138): nan->0, +-inf -> +-float32 max."""
+    return np.nan_to_num(g, nan=0.0, posinf=np.finfo(np.float32).max, neginf=np.finfo(np.float32).min).astype(F32)
+
+
+def step_size_of(step_lr, sigma, sigma_last):
+    """KITTISampling.py:135: step_lr * (sigma / sigmas[-1]) ** 2 in numpy float32."""
+    return F32(step_lr) * (F32(sigma) / F32(sigma_last)) ** 2
+
+
+def langevin_update(x, g, ref, mask, noise, step_size, grad_ref):
+    """x + s*g + r*(-mask*(x-ref)) + noise*sqrt(2s), float32, reference evaluation order."""
+    s = F32(step_size)
+    lik = (-mask).astype(F32) * (x - ref)
+    return (((x + s * g) + F32(grad_ref) * lik) + noise * F32(np.sqrt(F32(s * F32(2))))).astype(F32), lik
+
+
+# ----------------------------------------------------------------------------- samplers
+def sampler_baseline(x, ref, mask, score, sigmas, n_steps_each, step_lr, noise_fn, denoise=True, grad_ref=1.0):
+    """anneal_Langevin_dynamics_inpainting (models/__init__.py:1385-1442); returns images list."""
+    images = []
+    lik = None
+    for c, sigma in enumerate(sigmas):
+        s = step_size_of(step_lr, sigma, sigmas[-1])
+        for _ in range(n_steps_each):
+            gr = score(x, np.full(x.shape[0], c, np.int64))
+            x, lik = langevin_update(x, gr, ref, mask, noise_fn(x.shape), s, grad_ref)
+            images.append(x.copy())
+    if denoise:
+        gr = score(x, np.full(x.shape[0], len(sigmas) - 1, np.int64))
+        x = ((x + F32(sigmas[-1]) ** 2 * gr) + F32(grad_ref) * lik).astype(F32)
+        images.append(x.copy())
+    lik = (-mask).astype(F32) * (x - ref)
+    x = (x + F32(grad_ref) * lik).astype(F32)
+    images.append(x.copy())
+    return images
+
+
+def sampler_kitti(x, ref, mask, sky, min_step, setting, allowance, score, sigmas, fromWorld, toWorld, aB,
+                  n_steps_each, step_lr, exist, noise_fn, denoise=True, grad_ref=1.0, cc=0.01):
+    """anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti (KITTISampling.py:6-513)."""
+    images, shared = [], []
+    lik = None
+    for c, sigma in enumerate(sigmas):
+        if setting == 6:
+            cc = 1 / (len(sigmas) / (c + 1))
+        if setting == 7:
+            cc = 0.5 / (len(sigmas) / (c + 1))
+        s = step_size_of(step_lr, sigma, sigmas[-1])
+        for _ in range(n_steps_each):
+            gr = nan_to_num(score(x, np.full(x.shape[0], c, np.int64)))
+            x, lik = langevin_update(x, gr, ref, mask, noise_fn(x.shape), s, grad_ref)
+            if c >= min_step:
+                new, x = kitti_merge(x, mask, sky, exist, toWorld, fromWorld, aB, sigma, setting, allowance, cc)
+                if c in (0, 20, 110):
+                    shared.append(new)
+                if c == len(sigmas) - 1:
+                    images.append(new)
+    if denoise:
+        gr = score(x, np.full(x.shape[0], len(sigmas) - 1, np.int64))
+        x = ((x + F32(sigmas[-1]) ** 2 * gr) + F32(grad_ref) * lik).astype(F32)
+    lik = (-mask).astype(F32) * (x - ref)
+    x = (x + F32(grad_ref) * lik).astype(F32)
+    images.append(x)
+    return images, [], shared

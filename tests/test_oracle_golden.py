@@ -1,0 +1,170 @@
+"""Pin the CPU oracle to the reference's own outputs (tests/golden, made by oracle/gen_golden.py)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import golden_inputs as GI
+from oracle import sampling_ref as S
+from oracle import scorenet_ref as R
+from oracle.gen_golden import CIRCLE_MODS, MERGE_CASES
+from sdp.weights import get_sigmas_np, synthetic_state_dict
+
+torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+
+def _g(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+@pytest.fixture(scope="module")
+def params128():
+    return R.to_torch_params(synthetic_state_dict(128))
+
+
+def test_exist_mask_fixture():
+    ex = GI.exist_mask_full()
+    assert ex.shape == (64, 1024) and 0.5 < ex.mean() < 0.8
+
+
+@pytest.mark.parametrize("tag,B,H,W", [("ngf128_b2_64x256", 2, 64, 256), ("ngf128_b1_64x1024", 1, 64, 1024)])
+def test_scorenet_oracle_matches_reference(params128, tag, B, H, W):
+    f = _g(f"scorenet_{tag}.npz")
+    x = torch.from_numpy(GI.scorenet_input(tag, B, H, W))
+    with torch.no_grad():
+        out = R.scorenet_forward(params128, x, torch.from_numpy(f["y"])).numpy()
+    # same float32 ops in the same order -> bitwise equal on this CPU; allow 1e-6 of max
+    for b in range(B):
+        assert np.abs(out[b] - f["out"][b]).max() <= 1e-6 * np.abs(f["out"][b]).max()
+
+
+def test_ops_oracle_matches_reference():
+    import torch.nn.functional as F
+    from sdp.weights import synthetic_param
+    f = _g("ops_small.npz")
+    r = GI.rng("ops")
+    x = torch.from_numpy(r.standard_normal((2, 8, 16, 64)).astype(np.float32))
+    xs = torch.from_numpy(r.standard_normal((2, 8, 8, 32)).astype(np.float32))
+
+    def P(prefix, names_shapes):
+        return {f"{prefix}.{k}": torch.from_numpy(synthetic_param(f"{prefix}.{k}", s)) for k, s in names_shapes}
+
+    got = {}
+    p = P("op.inpp", [("alpha", (8,)), ("gamma", (8,)), ("beta", (8,))])
+    got["in_pp"] = R.instance_norm_pp(x, p, "op.inpp")
+    p = P("op.conv", [("weight", (8, 8, 3, 3)), ("bias", (8,))])
+    got["conv3x3_circ"] = R.conv2d(x, p["op.conv.weight"], p["op.conv.bias"])
+    for d in (2, 4):
+        p = P(f"op.dil{d}", [("weight", (8, 8, 3, 3)), ("bias", (8,))])
+        got[f"conv3x3_dil{d}"] = R.conv2d(x, p[f"op.dil{d}.weight"], p[f"op.dil{d}.bias"], dilation=d)
+    for k in (3, 1):
+        p = P(f"op.cmp{k}", [("conv.weight", (16, 8, k, k)), ("conv.bias", (16,))])
+        got[f"convmeanpool{k}"] = R.mean_pool2(R.conv2d(x, p[f"op.cmp{k}.conv.weight"], p[f"op.cmp{k}.conv.bias"],
+                                                        circular=False))
+    p = P("op.crp", [("convs.0.weight", (8, 8, 3, 3)), ("convs.1.weight", (8, 8, 3, 3))])
+    got["crp"] = R.crp(x, p, "op.crp")
+    p = P("op.rcu", [(f"{i}_{j}_conv.weight", (8, 8, 3, 3)) for i in (1, 2) for j in (1, 2)])
+    got["rcu"] = R.rcu(x, p, "op.rcu", 2)
+    p = P("op.msf", [("convs.0.weight", (8, 8, 3, 3)), ("convs.0.bias", (8,)),
+                     ("convs.1.weight", (8, 8, 3, 3)), ("convs.1.bias", (8,))])
+    got["msf"] = R.msf([x, xs], p, "op.msf", (16, 64))
+    names = [("normalize1.alpha", (8,)), ("normalize1.gamma", (8,)), ("normalize1.beta", (8,)),
+             ("conv1.weight", (8, 8, 3, 3)), ("conv1.bias", (8,)),
+             ("normalize2.alpha", (8,)), ("normalize2.gamma", (8,)), ("normalize2.beta", (8,)),
+             ("conv2.conv.weight", (16, 8, 3, 3)), ("conv2.conv.bias", (16,)),
+             ("shortcut.conv.weight", (16, 8, 1, 1)), ("shortcut.conv.bias", (16,))]
+    got["resblock_down"] = R.residual_block(x, P("op.rbd", names), "op.rbd", 8, 16, True, None)
+    for k, v in got.items():
+        np.testing.assert_allclose(v.detach().numpy(), f[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_langevin_oracle_matches_reference():
+    f = _g("langevin_step.npz")
+    case = GI.merge_case("langevin", 2, 64, 256)
+    g = GI.rng("langevin-grad").standard_normal((2, 2, 64, 256)).astype(np.float32) * 3.0
+    g[0, 0, 0, :4] = [np.nan, np.inf, -np.inf, 0.0]
+    sig = get_sigmas_np()[100:101]
+    s = S.step_size_of(6.2e-6, sig[0], sig[-1])
+    x1, _ = S.langevin_update(case["x"], g, case["ref"], case["mask"], GI.noise("langevin", 0, g.shape), s, 1.0)
+    np.testing.assert_array_equal(x1, f["x1"])  # bit exact (incl. the NaN/inf lanes)
+
+
+def _after_update(case):
+    x = case["x"]
+    return (x + (-case["mask"]).astype(np.float32) * (x - case["ref"])).astype(np.float32)
+
+
+def _final_dc(x, case):
+    return (x + (-case["mask"]).astype(np.float32) * (x - case["ref"])).astype(np.float32)
+
+
+@pytest.mark.parametrize("case_def", MERGE_CASES, ids=[c[0] for c in MERGE_CASES])
+def test_kitti_merge_oracle_matches_reference(case_def):
+    tag, B, aB, H, W, sigma, kw = case_def
+    case = GI.merge_case(tag, B, H, W, **kw)
+    f = _g(f"merge_{tag}.npz")
+    new, xc = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                            case["fromWorld"], aB, sigma)
+    np.testing.assert_allclose(new, f["new"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(_final_dc(xc, case), f["x"], rtol=1e-5, atol=1e-6)
+    assert ((new != 0) == (f["new"] != 0)).all()
+
+
+def test_identity_pose_row_shift():
+    """Appendix B.1: with identity poses output row r+1 is fed by source row r, row 0 is empty."""
+    case = GI.merge_case("k_b2a2_ident", 2, 64, 256, identity=True, neg_frac=0.0)
+    new, _ = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                           case["fromWorld"], 2, 0.5)
+    assert (new[:, :, 0] == 0).all()
+    assert (new[:, 0, 1:] != 0).mean() > 0.5
+
+
+@pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5)])
+def test_allforone_merge_oracle_matches_reference(tag, setting):
+    case = GI.merge_case(tag, 7, 64, 256)
+    f = _g(f"merge_{tag}.npz")
+    cc = 1 / (1 / 1) if setting == 5 else 0.01   # models/__init__.py:209-212 ramp at L=1, c=0
+    new, xc = S.allforone_merge(_after_update(case), case["mask"], case["sky"], case["exist"], CIRCLE_MODS, 7, 0.5,
+                                setting, cc)
+    np.testing.assert_allclose(new, f["new"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(_final_dc(xc, case), f["x"], rtol=1e-5, atol=1e-6)
+
+
+def _score_fn(params):
+    def score(x, y):
+        with torch.no_grad():
+            return R.scorenet_forward(params, torch.from_numpy(x), torch.from_numpy(y)).numpy()
+    return score
+
+
+def _noise_feed(tag):
+    k = [0]
+
+    def fn(shape):
+        n = GI.noise(tag, k[0], shape)
+        k[0] += 1
+        return n
+    return fn
+
+
+def test_config1_baseline_sampler(params128):
+    f = _g("config1_b1_64x256.npz")
+    case = GI.merge_case("config1", 1, 64, 256)
+    x0 = GI.scorenet_input("config1", 1, 64, 256)
+    imgs = S.sampler_baseline(x0, case["ref"], case["mask"], _score_fn(params128), get_sigmas_np()[:1], 5, 6.2e-6,
+                              _noise_feed("config1"))
+    for k, i in (("step1", 0), ("step5", 4), ("denoised", 5), ("final", 6)):
+        np.testing.assert_allclose(imgs[i], f[k], rtol=1e-5, atol=1e-5, err_msg=k)
+
+
+def test_kitti_sampler_end_to_end(params128):
+    f = _g("kitti_e2e_b2_64x256.npz")
+    case = GI.merge_case("e2e", 2, 64, 256)
+    x0 = GI.scorenet_input("e2e", 2, 64, 256)
+    images, _, _ = S.sampler_kitti(x0, case["ref"], case["mask"], case["sky"], 2, 5, 10, _score_fn(params128),
+                                   get_sigmas_np()[229:232], case["fromWorld"], case["toWorld"], 2, 2, 6.2e-6,
+                                   case["exist"], _noise_feed("e2e"))
+    np.testing.assert_allclose(images[0], f["new"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(images[1], f["final"], rtol=1e-5, atol=1e-5)
