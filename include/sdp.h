@@ -1,0 +1,114 @@
+/*
+ * sdp.h -- C ABI of libsdp.so, the MI355X (gfx950) implementation of the
+ * Simultaneous-Diffusion-for-Pointclouds sampling hot path.
+ *
+ * Every pointer argument named x/grad/ref/... is a DEVICE pointer owned by the caller
+ * unless documented otherwise; every call is enqueued on the caller's hipStream_t
+ * (passed as void*) and never synchronises the device.  Return value: 0 = OK,
+ * < 0 = error; sdp_last_error() gives a thread-local message for the last failure.
+ * Handles are per device and not thread-safe: one handle per (device, thread).
+ *
+ * Reference interfaces replaced (paths relative to /root/reference/LiDARGen):
+ *   sdp_net_*              scorenet(x, y) = NCSN_LiDAR_small.forward   models/ncsnv2.py:420-518
+ *                          weight load    load_state_dict + EMAHelper  runners/ncsn_runner_kitti_simultaneous.py:472-489
+ *   sdp_langevin_step      Langevin update                           models/KITTISampling.py:133-156,
+ *                                                                     models/__init__.py:236-259, :1397-1416
+ *   sdp_consistency_merge  cross-view reprojection + correction      models/KITTISampling.py:160-490 (pose matrices),
+ *                                                                     models/__init__.py:263-579 (origin offsets)
+ */
+#ifndef SDP_H
+#define SDP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDP_VERSION 100  /* 1.0.0 */
+
+/* arithmetic used for the score network's convolutions (fp32 I/O and accumulation in all modes) */
+enum sdp_precision {
+  SDP_PREC_FP32 = 0,    /* v_mfma_f32_32x32x2_f32: exact fp32 products                         */
+  SDP_PREC_FP32X3 = 1,  /* 3-pass bf16 split (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_bf16 */
+  SDP_PREC_BF16 = 2     /* single bf16 pass (fast, NOT within the fp32 parity tolerance)        */
+};
+
+typedef struct sdp_net_desc {
+  int ngf;          /* 128 (NCSN_LiDAR_small config.model.ngf)                    */
+  int channels;     /* 2 (depth, intensity)                                        */
+  int H, W;         /* 64, 1024 (config.data.image_size / image_width)             */
+  int num_classes;  /* 232 (length of the model's sigma buffer)                    */
+  int precision;    /* enum sdp_precision                                          */
+} sdp_net_desc;
+
+typedef struct sdp_net sdp_net;
+
+int sdp_version(void);
+const char* sdp_last_error(void);
+
+/* ---- score network (NCSN_LiDAR_small) ------------------------------------------------ */
+int sdp_net_create(const sdp_net_desc* desc, sdp_net** out);
+/* Copy one state_dict tensor (HOST float32, reference key and shape, e.g. "res1.0.conv1.weight"
+ * [128,128,3,3] or "sigmas" [232]).  The library owns its copy after the call. */
+int sdp_net_set_param(sdp_net* net, const char* key, const float* host_data, const int64_t* shape, int ndim);
+/* Check every parameter was set and upload the device layouts (blocking; call once). */
+int sdp_net_finalize(sdp_net* net);
+int sdp_net_workspace_size(const sdp_net* net, int B, size_t* bytes);
+/* out[B,2,H,W] = scorenet(x[B,2,H,W], labels[B]) ; labels: int64 device array indexing sigmas. */
+int sdp_net_forward(sdp_net* net, const float* x, const int64_t* labels, float* out, int B,
+                    void* workspace, size_t workspace_bytes, void* stream);
+int sdp_net_destroy(sdp_net* net);
+/* Measurement hooks: when enabled, every conv launch of sdp_net_forward is bracketed by HIP
+ * events on the forward's stream; sdp_net_profile_read synchronises on them and writes one
+ * line per conv class: "class\tlaunches\ttotal_ms\tflops_per_launch\n". */
+int sdp_net_profile_enable(sdp_net* net, int enable);
+int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches);
+
+/* ---- Langevin update ------------------------------------------------------------------ *
+ * x <- x + step*g' + grad_ref*lik + noise*noise_scale   (float32, reference evaluation order)
+ *   g'  = nan_to_num(grad) if nan_to_num else grad;  lik = -mask*(x - ref)
+ *   noise = noise_or_null[i] if given, else N(0,1) from Philox4x32-10(seed, counter = offset + i/4)
+ * Optional outputs: lik_out (the step's grad_likelihood, used by the denoise step) and
+ * absmax_bits: atomicMax of |x_new[:,0]| float bits (the merge's tooHigh input).          */
+int sdp_langevin_step(float* x, const float* grad, const float* ref, const int32_t* mask,
+                      const float* noise_or_null, uint64_t seed, uint64_t offset,
+                      float step_size, float noise_scale, float grad_ref, int nan_to_num,
+                      int B, int C, int HW, float* lik_out, uint32_t* absmax_bits, void* stream);
+/* x <- x + a*g + b*lik   (denoise: a = sigma_L^2, b = grad_ref) ; x <- x + b*(-mask*(x-ref)) if g == NULL */
+int sdp_axpy_step(float* x, const float* g, float a, const float* lik, const int32_t* mask,
+                  const float* ref, float b, int n, void* stream);
+
+/* ---- cross-view consistency merge ----------------------------------------------------- */
+enum sdp_merge_variant { SDP_MERGE_POSES = 0, SDP_MERGE_ORIGINS = 1 };
+
+typedef struct sdp_merge_params {
+  int variant;            /* enum sdp_merge_variant                                        */
+  int setting;            /* 5 (kitti min-depth filter) / 7 (AllForOne controlled average) */
+  float sigma;            /* current sigma (float32 from the sigma array)                  */
+  float allowance;        /* metres (10)                                                   */
+  float cc;               /* correlation coefficient                                       */
+} sdp_merge_params;
+
+int sdp_merge_workspace_size(int n_src, int n_out, int H, int W, size_t* bytes);
+/*
+ * x_all   : [n_src,2,H,W] current images of every source view (device, float32)
+ * toWorld : [n_src,4,4] float64 (POSES) ; fromWorld : [n_src,4,4] float64 (POSES)
+ * origins : [aB,3] float32 view origins (ORIGINS variant; models/__init__.py:224-231)
+ * exist   : [aB,H,W] uint8 (existMask[:aB]) ; sky : [n_src,H,W] uint8 ; refmask : [n_src,2,H,W] int32
+ * Views are grouped into megabatches of aB consecutive indices.  Output views are
+ * [o_begin, o_begin+n_out); their images in x_all are corrected in place.
+ * absmax_bits : device word holding max|x[:,0]| bits over ALL views of the step (tooHigh).
+ * new_images  : optional [n_out,2,H,W] float32 output (the reference's newImages).
+ */
+int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_out, int H, int W,
+                          const double* toWorld, const double* fromWorld, const float* origins,
+                          const uint8_t* exist, const uint8_t* sky, const int32_t* refmask,
+                          const sdp_merge_params* params, const uint32_t* absmax_bits,
+                          float* new_images, void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,233 @@
+// Small / memory-bound kernels of the score network (gfx950).
+//   begin_conv : input prep (2x-1, coordinate channels; ncsnv2.py:485-496) fused with the
+//                4->ngf zero-padded 3x3 conv + bias (ncsnv2.py:433,498) and IN++ tile stats.
+//   end_conv   : final IN++ affine + ELU prologue, ngf->2 zero-padded 3x3 conv + bias,
+//                / sigmas[y] (ncsnv2.py:510-516), NCHW output.
+//   inpp_finalize : per-tile (mean, M2) -> per-(b,c) InstanceNorm2dPlus scale/shift
+//                (normalization.py:163-176).
+//   maxpool5   : MaxPool2d(5, stride 1, padding 2) of CRPBlock (layers.py:70), NHWC.
+#include "common.h"
+
+namespace sdp {
+
+// torch.linspace(0, 1, steps=n)[i] (scalar form: start + step*i below halfway, else end - step*(n-1-i))
+SDP_DEV float linspace01(int i, int n) {
+  if (n == 1) return 0.f;
+  const float step = 1.0f / (float)(n - 1);
+  return i < n / 2 ? step * (float)i : 1.0f - step * (float)(n - 1 - i);
+}
+
+SDP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ---------------------------------------------------------------- begin conv (Cin=4 -> 128)
+// block: 64 output pixels of one row x 128 channels; thread = (pixel, 32-channel quarter)
+__global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                         const float* __restrict__ bias, float* __restrict__ out,
+                                                         float* __restrict__ stats, int H, int W) {
+  constexpr int CO = 128;
+  __shared__ float sw[36 * CO];          // [ci*9 + tap][co]
+  __shared__ float sp[4][3][66];         // prepped input patch [ci][row][col]
+  const int tid = threadIdx.x;
+  const int tiles_row = W / 64;
+  const int tiles_per_img = H * tiles_row;
+  const int b = blockIdx.x / tiles_per_img, tile = blockIdx.x % tiles_per_img;
+  const int y = tile / tiles_row, x0 = (tile % tiles_row) * 64;
+  for (int i = tid; i < 36 * CO; i += 256) {
+    const int co = i % CO, k = i / CO;          // k = ci*9 + tap ; w is [co][ci][3][3]
+    sw[i] = w[co * 36 + k];
+  }
+  for (int i = tid; i < 4 * 3 * 66; i += 256) {
+    const int ci = i / 198, r = (i / 66) % 3, c = i % 66;
+    const int yy = y - 1 + r, xx = x0 - 1 + c;
+    float v = 0.f;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+      if (ci < 2) v = 2.f * x[(((size_t)b * 2 + ci) * H + yy) * W + xx] - 1.f;
+      else if (ci == 2) v = linspace01(xx, W);
+      else v = linspace01(yy, H);
+    }
+    sp[ci][r][c] = v;
+  }
+  __syncthreads();
+  const int px = tid & 63, cq = tid >> 6;
+  float acc[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) acc[j] = bias[cq * 32 + j];
+  for (int ci = 0; ci < 4; ++ci)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const float v = sp[ci][tap / 3][px + tap % 3];
+      const float* wr = sw + (ci * 9 + tap) * CO + cq * 32;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) acc[j] = fmaf(v, wr[j], acc[j]);
+    }
+  float* o = out + (((size_t)b * H + y) * W + x0 + px) * CO + cq * 32;
+#pragma unroll
+  for (int j = 0; j < 32; j += 4) *reinterpret_cast<float4*>(o + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+  // per-(b, co) stats of this 64-pixel tile: one wave holds all 64 pixels of its 32 channels
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const float mean = wave_sum(acc[j]) * (1.0f / 64.f);
+    const float dv = acc[j] - mean;
+    const float m2 = wave_sum(dv * dv);
+    if (px == j) {
+      float2* st = reinterpret_cast<float2*>(stats) + ((size_t)b * tiles_per_img + tile) * CO + cq * 32 + j;
+      *st = make_float2(mean, m2);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- end conv (128 -> 2), NCHW out
+// block: 4 rows x 64 cols of output; LDS patch of one 32-channel chunk, pixel stride 33 floats
+__global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__ in, const float* __restrict__ ss,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       const float* __restrict__ sigmas, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ out, int H, int W, int Cin) {
+  constexpr int PS = 33;
+  __shared__ float sp[6 * 66 * PS];
+  __shared__ float sw[2 * 32 * 9];   // [co][ci][tap] of the chunk
+  const int tid = threadIdx.x;
+  const int tiles_row = W / 64, tiles_per_img = (H / 4) * tiles_row;
+  const int b = blockIdx.x / tiles_per_img, tile = blockIdx.x % tiles_per_img;
+  const int y0 = (tile / tiles_row) * 4, x0 = (tile % tiles_row) * 64;
+  const int r = tid >> 6, c = tid & 63;
+  const float* ssb = ss + (size_t)b * Cin * 2;
+  float a0 = 0.f, a1 = 0.f;
+  for (int c0 = 0; c0 < Cin; c0 += 32) {
+    __syncthreads();
+    for (int i = tid; i < 6 * 66 * 8; i += 256) {
+      const int pix = i >> 3, cv = i & 7;
+      const int pr = pix / 66, pc = pix % 66;
+      const int yy = y0 - 1 + pr, xx = x0 - 1 + pc;
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const int ch = c0 + cv * 4;
+        const float4 f = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * Cin + ch);
+        const float fv[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = elu(fmaf(fv[k], ssb[(ch + k) * 2], ssb[(ch + k) * 2 + 1]));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sp[pix * PS + cv * 4 + k] = v[k];
+    }
+    for (int i = tid; i < 2 * 32 * 9; i += 256) {
+      const int co = i / 288, rem = i % 288, ci = rem / 9, tap = rem % 9;
+      sw[i] = w[((size_t)co * Cin + c0 + ci) * 9 + tap];
+    }
+    __syncthreads();
+    for (int ci = 0; ci < 32; ++ci)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const float v = sp[((r + tap / 3) * 66 + c + tap % 3) * PS + ci];
+        a0 = fmaf(v, sw[ci * 9 + tap], a0);
+        a1 = fmaf(v, sw[288 + ci * 9 + tap], a1);
+      }
+  }
+  const float sg = sigmas[labels[b]];
+  const int yy = y0 + r, xx = x0 + c;
+  out[(((size_t)b * 2 + 0) * H + yy) * W + xx] = (a0 + bias[0]) / sg;
+  out[(((size_t)b * 2 + 1) * H + yy) * W + xx] = (a1 + bias[1]) / sg;
+}
+
+// ---------------------------------------------------------------- IN++ finalize
+// stats [B][T][C] of float2 (tile mean, tile M2) with `cnt` values per tile -> ss [B][C] of
+// float2 (scale, shift) such that IN++(x) = x*scale + shift.
+__global__ void inpp_finalize_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
+                                     const float* __restrict__ alpha, const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, float2* __restrict__ ss) {
+  __shared__ double red[256];
+  const int b = blockIdx.x, c = threadIdx.x;
+  const float2* st = stats + (size_t)b * T * C + c;
+  double sm = 0.0;
+  for (int t = 0; t < T; ++t) sm += st[(size_t)t * C].x;
+  const double mean = sm / T;
+  double m2 = 0.0;
+  for (int t = 0; t < T; ++t) {
+    const float2 v = st[(size_t)t * C];
+    const double dm = (double)v.x - mean;
+    m2 += (double)v.y + dm * dm * cnt;
+  }
+  const double var = m2 / ((double)T * cnt);          // biased (nn.InstanceNorm2d)
+  // m = mean_c(mean), v = unbiased var_c(mean)       (normalization.py:164-166)
+  red[c] = mean;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (c < s) red[c] += red[c + s];
+    __syncthreads();
+  }
+  const double m = red[0] / C;
+  __syncthreads();
+  red[c] = (mean - m) * (mean - m);
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (c < s) red[c] += red[c + s];
+    __syncthreads();
+  }
+  const double v = red[0] / (C - 1);
+  const double inv = 1.0 / sqrt(var + 1e-5);
+  const double mn = (mean - m) / sqrt(v + 1e-5);
+  const double g = gamma[c];
+  const double scale = g * inv;
+  const double shift = g * (-mean * inv + mn * (double)alpha[c]) + (double)beta[c];
+  ss[(size_t)b * C + c] = make_float2((float)scale, (float)shift);
+}
+
+// ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
+__global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                       int B, int H, int W, int C) {
+  const int C4 = C / 4;
+  const size_t n = (size_t)B * H * W * C4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    size_t p = i / C4;
+    const int x = p % W;
+    p /= W;
+    const int y = p % H;
+    const int b = p / H;
+    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    for (int dy = -2; dy <= 2; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= H) continue;
+      for (int dx = -2; dx <= 2; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= W) continue;
+        const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
+        m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+      }
+    }
+    *reinterpret_cast<float4*>(out + i * 4) = m;
+  }
+}
+
+// ---------------------------------------------------------------- host launchers
+hipError_t begin_conv(const float* x, const float* w, const float* bias, float* out, float* stats, int B, int H, int W,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(begin_conv_kernel, dim3(B * H * (W / 64)), dim3(256), 0, st, x, w, bias, out, stats, H, W);
+  return hipGetLastError();
+}
+
+hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
+                    const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st) {
+  hipLaunchKernelGGL(end_conv_kernel, dim3(B * (H / 4) * (W / 64)), dim3(256), 0, st, in, ss, w, bias, sigmas, labels,
+                     out, H, W, Cin);
+  return hipGetLastError();
+}
+
+hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
+                         const float* beta, float* ss, hipStream_t st) {
+  hipLaunchKernelGGL(inpp_finalize_kernel, dim3(B), dim3(C), 0, st, reinterpret_cast<const float2*>(stats), T, cnt, C,
+                     alpha, gamma, beta, reinterpret_cast<float2*>(ss));
+  return hipGetLastError();
+}
+
+hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st) {
+  const size_t n = (size_t)B * H * W * (C / 4);
+  const int grid = (int)std::min<size_t>((n + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(maxpool5_kernel, dim3(grid), dim3(256), 0, st, in, out, B, H, W, C);
+  return hipGetLastError();
+}
+
+}  // namespace sdp

@@ -1,0 +1,37 @@
+// Shared device helpers and launch-argument structs for libsdp (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define SDP_DEV __device__ __forceinline__
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+namespace sdp {
+
+enum { MODE_F32 = 0, MODE_F32X3 = 1, MODE_BF16 = 2 };
+enum { PRO_NONE = 0, PRO_ELU = 1, PRO_AFFINE_ELU = 2 };
+
+// nn.ELU(alpha=1) (LiDARGen/models/layers.py:11-13)
+SDP_DEV float elu(float x) { return x > 0.f ? x : (__expf(x) - 1.0f); }
+
+// Arguments of one implicit-GEMM 3x3 / 1x1 convolution launch (activations NHWC float32).
+struct ConvArgs {
+  const float* in;         // [B][H][W][Cin]
+  const uint4* wf;         // fragment-ordered weights (see net.cpp pack_conv_weights)
+  const float* bias;       // [Cout] or null
+  float* out;              // [B][Ho][Wo][Cout]  (Ho,Wo = H,W or H/2,W/2 when pooled)
+  const float* res;        // residual, layout of out, or null
+  float* out2;             // optional second output: value + res2 (CRP running sum)
+  const float* res2;
+  const float* up;         // [B][H/2][W/2][Cout]: bilinear(align_corners) upsample-add, or null
+  const float* pro_ss;     // [B][Cin][2] (scale, shift) for PRO_AFFINE_ELU
+  float* stats;            // [B][tiles_per_img][Cout][2] per-tile (mean, M2) or null
+  int B, H, W, Cin, Cout;
+  int dil, circular, pro_mode, epi_elu;
+  int tiles_per_img;
+};
+
+}  // namespace sdp

@@ -1,0 +1,39 @@
+// Merge launch arguments (see merge.hip).
+#pragma once
+#include "common.h"
+
+namespace sdp {
+
+struct MergeGeom {
+  double hA, vA, hMin, bigMin;
+  int H, W, big;
+};
+
+struct MergeArgs {
+  const float* x;          // [n_src][2][HW]
+  const double* toWorld;   // [n_src][16]  (POSES)
+  const double* fromWorld; // [n_src][16]  (POSES)
+  const float* origins;    // [aB][3]      (ORIGINS)
+  const uint8_t* exist;    // [aB][HW]
+  const uint8_t* sky;      // [n_src][HW]
+  const int32_t* refmask;  // [n_src][2][HW]
+  const double* trig;      // cos_az[W], sin_az[W], cos_el[H], sin_el[H]
+  double4* world;          // [n_src][HW] world point + source-valid flag
+  uint32_t* cnt;           // [n_out][cells]
+  uint32_t* minidx;
+  double* sumL;
+  double* sumI;
+  unsigned long long* minkey;
+  float* newimg;           // [n_out][2][HW]
+  uint8_t* maskimg;        // [n_out][HW]
+  const uint32_t* absmax;  // max |x[:,0]| bits over all views
+  float* xout;             // x_all (corrected in place for the output views)
+  MergeGeom g;
+  int n_src, aB, o_begin, n_out, variant, setting;
+  float smod, allowance, cc, min_code;
+};
+
+size_t merge_ws_bytes(int n_src, int n_out, int H, int W);
+hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why);
+
+}  // namespace sdp

@@ -1,0 +1,529 @@
+// Score-network runtime: parameter store, weight packing and the forward plan of
+// NCSN_LiDAR_small (LiDARGen/models/ncsnv2.py:420-518) over the libsdp kernels.
+//
+// Activations live in HBM as NHWC float32 carved from the caller's workspace; every
+// InstanceNorm++ is split into per-tile statistics written by the producing conv's
+// epilogue + a tiny finalize kernel + an affine/ELU prologue in the consuming conv, so no
+// activation is ever re-read just for normalisation.
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sdp.h"
+#include "kernels.h"
+
+namespace sdp {
+
+struct HostParam {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+static uint16_t f2bf(float f) {  // round-to-nearest-even (finite inputs)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static float bf2f(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// Weight W[Cout][Cin][k][k] -> MFMA fragment order consumed by conv_mfma_kernel:
+//   [chunk = Cin/32][tap][nb = Cout/32][lane 64][16 x 4 bytes]
+// F32  : slot q of lane l = W[nb*32 + (l&31)][chunk*32 + 16*(l>>5) + q]
+// BF16 : slots = [s][hi 8 | lo 8] ; element j of lane l = ci chunk*32 + 16*s + 8*(l>>5) + j
+static std::vector<uint32_t> pack_conv_weights(const HostParam& p, int mode) {
+  const int Cout = (int)p.shape[0], Cin = (int)p.shape[1], k = (int)p.shape[2];
+  const int NT = k * k, NB = Cout / 32, NC = Cin / 32;
+  std::vector<uint32_t> out((size_t)Cout * Cin * NT);
+  for (int ch = 0; ch < NC; ++ch)
+    for (int tap = 0; tap < NT; ++tap)
+      for (int nb = 0; nb < NB; ++nb)
+        for (int lane = 0; lane < 64; ++lane) {
+          uint32_t* dst = &out[((((size_t)ch * NT + tap) * NB + nb) * 64 + lane) * 16];
+          const int co = nb * 32 + (lane & 31), h = lane >> 5;
+          auto wv = [&](int ci) { return p.data[((size_t)co * Cin + ci) * NT + tap]; };
+          if (mode == SDP_PREC_FP32) {
+            for (int q = 0; q < 16; ++q) {
+              const float f = wv(ch * 32 + 16 * h + q);
+              std::memcpy(&dst[q], &f, 4);
+            }
+          } else {
+            uint16_t* d16 = reinterpret_cast<uint16_t*>(dst);
+            for (int s = 0; s < 2; ++s)
+              for (int j = 0; j < 8; ++j) {
+                const float f = wv(ch * 32 + 16 * s + 8 * h + j);
+                const uint16_t hi = f2bf(f);
+                const uint16_t lo = f2bf(f - bf2f(hi));
+                d16[s * 16 + j] = hi;
+                d16[s * 16 + 8 + j] = lo;
+              }
+          }
+        }
+  return out;
+}
+
+}  // namespace sdp
+
+using namespace sdp;
+
+struct ProfRec {
+  std::string cls;
+  double flops;
+  hipEvent_t a, b;
+};
+
+struct sdp_net {
+  sdp_net_desc d;
+  bool profile = false;
+  std::vector<ProfRec> prof;        // events of the forwards since the last read
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, HostParam> host;
+  std::map<std::string, void*> dev;  // plain tensors and packed conv weights ("#frag" suffix)
+  bool finalized = false;
+  int mode = MODE_F32X3;
+
+  ~sdp_net() {
+    for (auto& kv : dev) (void)hipFree(kv.second);
+    for (auto& r : prof) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+  }
+  hipEvent_t event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
+    return e;
+  }
+  const float* P(const std::string& k) const {
+    auto it = dev.find(k);
+    if (it == dev.end()) throw std::runtime_error("missing parameter " + k);
+    return reinterpret_cast<const float*>(it->second);
+  }
+  const float* Pn(const std::string& k) const {  // optional
+    auto it = dev.find(k);
+    return it == dev.end() ? nullptr : reinterpret_cast<const float*>(it->second);
+  }
+};
+
+namespace {
+
+void chk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct Buf {
+  float* p;
+  int H, W, C;
+};
+
+struct Fwd {
+  sdp_net* net;
+  int B;
+  hipStream_t st;
+  float* stats;
+  float* ss;
+
+  struct Opt {
+    int pro = PRO_NONE;        // prologue
+    bool bias = true;
+    const float* res = nullptr;
+    const float* up = nullptr;
+    float* out2 = nullptr;
+    const float* res2 = nullptr;
+    bool epi_elu = false;
+    bool stats = false;
+    int dil = 1;
+    bool circular = true;
+    bool pool = false;
+  };
+
+  void conv(const Buf& in, const std::string& wkey, const Buf& out, const Opt& o) {
+    const auto& hp = net->host.at(wkey + ".weight");
+    ConvArgs a{};
+    a.in = in.p;
+    a.wf = reinterpret_cast<const uint4*>(net->P(wkey + ".weight#frag"));
+    a.bias = o.bias ? net->P(wkey + ".bias") : nullptr;
+    a.out = out.p;
+    a.res = o.res;
+    a.out2 = o.out2;
+    a.res2 = o.res2;
+    a.up = o.up;
+    a.pro_ss = o.pro == PRO_AFFINE_ELU ? ss : nullptr;
+    a.stats = o.stats ? stats : nullptr;
+    a.B = B;
+    a.H = in.H;
+    a.W = in.W;
+    a.Cin = in.C;
+    a.Cout = out.C;
+    a.dil = o.dil;
+    a.circular = o.circular ? 1 : 0;
+    a.pro_mode = o.pro;
+    a.epi_elu = o.epi_elu ? 1 : 0;
+    if ((int)hp.shape[1] != in.C || (int)hp.shape[0] != out.C) throw std::runtime_error("conv shape mismatch " + wkey);
+    const char* why = "conv launch";
+    const int ks = (int)hp.shape[2];
+    ProfRec rec;
+    if (net->profile) {
+      rec.cls = "conv" + std::to_string(ks) + "x" + std::to_string(ks) + " " + std::to_string(in.C) + "->" +
+                std::to_string(out.C) + " @" + std::to_string(in.H) + "x" + std::to_string(in.W) + " d" +
+                std::to_string(o.dil) + (o.pool ? " pool" : "");
+      rec.flops = 2.0 * B * in.H * in.W * (double)in.C * out.C * ks * ks;
+      rec.a = net->event();
+      rec.b = net->event();
+      chk(hipEventRecord(rec.a, st), "hipEventRecord");
+    }
+    hipError_t e = conv_mfma(net->mode, a, ks, o.pool, st, &why);
+    if (e != hipSuccess) throw std::runtime_error(std::string(why) + " (" + wkey + ")");
+    if (net->profile) {
+      chk(hipEventRecord(rec.b, st), "hipEventRecord");
+      net->prof.push_back(rec);
+    }
+  }
+
+  // stats (written by the previous conv) -> scale/shift of InstanceNorm2dPlus `nkey`
+  void norm(const std::string& nkey, int T, float cnt, int C) {
+    chk(inpp_finalize(stats, B, T, cnt, C, net->P(nkey + ".alpha"), net->P(nkey + ".gamma"), net->P(nkey + ".beta"), ss,
+                      st),
+        "inpp_finalize");
+  }
+  static int tiles(const Buf& b) { return b.H * b.W / 128; }
+
+  // ResidualBlock.forward (layers.py:443-456); returns output in `out`, stats of out written
+  void resblock(const std::string& k, const Buf& x, const Buf& t1, const Buf& t2, const Buf& out, bool down, int dil,
+                bool want_stats, int x_tiles, float x_cnt) {
+    norm(k + ".normalize1", x_tiles, x_cnt, x.C);
+    Opt o1;
+    o1.pro = PRO_AFFINE_ELU;
+    o1.stats = true;
+    o1.dil = dil;
+    conv(x, k + ".conv1", t1, o1);
+    norm(k + ".normalize2", tiles(t1), 128.f, t1.C);
+    Opt o2;
+    o2.pro = PRO_AFFINE_ELU;
+    o2.stats = want_stats;
+    o2.dil = dil;
+    if (down && dil == 1) {
+      // ConvMeanPool shortcut (1x1, zero pad) on the raw input, then conv2 = ConvMeanPool 3x3
+      Opt os;
+      os.circular = false;
+      os.pool = true;
+      conv(x, k + ".shortcut.conv", t2, os);
+      o2.circular = false;
+      o2.pool = true;
+      o2.res = t2.p;
+      conv(t1, k + ".conv2.conv", out, o2);
+    } else if (down) {
+      Opt os;
+      os.dil = dil;
+      conv(x, k + ".shortcut", t2, os);
+      o2.res = t2.p;
+      conv(t1, k + ".conv2", out, o2);
+    } else {
+      o2.res = x.p;
+      conv(t1, k + ".conv2", out, o2);
+    }
+  }
+
+  // RCUBlock (layers.py:126-134): n blocks of [ELU->conv->ELU->conv] + residual.
+  // Result in slots[last]; uses tmp.  epi_elu on the final conv when a CRP follows.
+  Buf rcu(const std::string& k, Buf x, int nblocks, const Buf& tmp, const Buf& o0, const Buf& o1, bool final_elu,
+          bool final_stats) {
+    Buf outs[2] = {o0, o1};
+    for (int i = 0; i < nblocks; ++i) {
+      Opt a;
+      a.pro = PRO_ELU;
+      a.bias = false;
+      conv(x, k + "." + std::to_string(i + 1) + "_1_conv", tmp, a);
+      Opt b;
+      b.pro = PRO_ELU;
+      b.bias = false;
+      b.res = x.p;
+      b.epi_elu = final_elu && i == nblocks - 1;
+      b.stats = final_stats && i == nblocks - 1;
+      const Buf& y = outs[i & 1];
+      conv(tmp, k + "." + std::to_string(i + 1) + "_2_conv", y, b);
+      x = y;
+    }
+    return x;
+  }
+
+  // CRPBlock (layers.py:76-83) on X = ELU(h) (already applied by the producer)
+  // -> returns x2 ; slots: P (pool), Q (path), R (x1), S (x2)
+  Buf crp(const std::string& k, const Buf& X, const Buf& P, const Buf& Qp, const Buf& R, const Buf& S) {
+    chk(maxpool5(X.p, P.p, B, X.H, X.W, X.C, st), "maxpool5");
+    Opt a;
+    a.bias = false;
+    a.out2 = R.p;
+    a.res2 = X.p;
+    conv(P, k + ".convs.0", Qp, a);                   // path1 -> Qp ; x1 = path1 + X -> R
+    chk(maxpool5(Qp.p, P.p, B, X.H, X.W, X.C, st), "maxpool5");
+    Opt b;
+    b.bias = false;
+    b.res = R.p;
+    conv(P, k + ".convs.1", S, b);                    // x2 = path2 + x1
+    return S;
+  }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ forward
+static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, float* out, int B, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
+  const int H = net->d.H, W = net->d.W, C = net->d.ngf, C2 = 2 * C;
+  const int h = H / 2, w = W / 2;
+  const size_t F = (size_t)B * H * W * C, Q = (size_t)B * h * w * C2;
+  char* p = reinterpret_cast<char*>(ws);
+  char* end = p + ws_bytes;
+  auto take = [&](size_t n) {
+    float* q = reinterpret_cast<float*>(p);
+    p += ((n * 4 + 255) / 256) * 256;
+    if (p > end) throw std::runtime_error("workspace too small");
+    return q;
+  };
+  Fwd f{net, B, st, nullptr, nullptr};
+  f.stats = take((size_t)B * (H * W / 64) * C2 * 2);
+  f.ss = take((size_t)B * C2 * 2);
+  auto full = [&]() { return Buf{take(F), H, W, C}; };
+  auto half = [&]() { return Buf{take(Q), h, w, C2}; };
+  Buf L1 = full(), FA = full(), FB = full(), FC = full(), FD = full(), FE = full();
+  Buf L2 = half(), L3 = half(), L4 = half(), QA = half(), QB = half(), QC = half(), QD = half(), QE = half();
+  auto half128 = [&](const Buf& b) { return Buf{b.p, h, w, C}; };
+
+  using Opt = Fwd::Opt;
+  // begin_conv + input prep  -> FA (stats over 64-px tiles)
+  chk(begin_conv(x, net->P("begin_conv.weight"), net->P("begin_conv.bias"), FA.p, f.stats, B, H, W, st), "begin_conv");
+  // res1
+  f.resblock("res1.0", FA, FB, FD, FC, false, 1, true, H * W / 64, 64.f);
+  f.resblock("res1.1", FC, FB, FD, L1, false, 1, true, Fwd::tiles(FC), 128.f);
+  // res2 (down: ConvMeanPool)
+  f.resblock("res2.0", L1, FB, QA, QB, true, 1, true, Fwd::tiles(L1), 128.f);
+  f.resblock("res2.1", QB, QA, QC, L2, false, 1, true, Fwd::tiles(L1), 32.f);
+  // res3 (dilation 2), res4 (dilation 4)
+  f.resblock("res3.0", L2, QA, QB, QC, true, 2, true, Fwd::tiles(L2), 128.f);
+  f.resblock("res3.1", QC, QA, QB, L3, false, 2, true, Fwd::tiles(QC), 128.f);
+  f.resblock("res4.0", L3, QA, QB, QC, true, 4, true, Fwd::tiles(L3), 128.f);
+  f.resblock("res4.1", QC, QA, QB, L4, false, 4, false, Fwd::tiles(QC), 128.f);
+
+  // refine1([L4]) : adapt RCU -> ELU -> CRP -> output RCU
+  Buf a1 = f.rcu("refine1.adapt_convs.0", L4, 2, QA, QB, QC, true, false);          // ELU(h) in QC
+  Buf x2 = f.crp("refine1.crp", a1, QA, QB, QD, QE);
+  Buf ref1 = f.rcu("refine1.output_convs", x2, 1, QA, QB, QC, false, false);       // QB
+  // refine2([L3, ref1]) ; ref1 lives in QB
+  Buf hA = f.rcu("refine2.adapt_convs.0", L3, 2, QA, QC, QD, false, false);        // QD
+  Buf hB = f.rcu("refine2.adapt_convs.1", ref1, 2, QA, QC, QE, false, false);      // QE
+  {
+    Opt o;
+    f.conv(hA, "refine2.msf.convs.0", QA, o);                                      // m0 -> QA
+    Opt o1;
+    o1.res = QA.p;
+    o1.epi_elu = true;
+    f.conv(hB, "refine2.msf.convs.1", QB, o1);                                     // ELU(m0 + m1) -> QB
+  }
+  x2 = f.crp("refine2.crp", QB, QA, QC, QD, QE);                                   // QE
+  Buf ref2 = f.rcu("refine2.output_convs", x2, 1, QA, QB, QC, false, false);       // QB
+  // refine3([L2, ref2]) -> 128 channels at half resolution
+  hA = f.rcu("refine3.adapt_convs.0", L2, 2, QA, QC, QD, false, false);            // QD
+  hB = f.rcu("refine3.adapt_convs.1", ref2, 2, QA, QC, QE, false, false);          // QE
+  {
+    Opt o;
+    f.conv(hA, "refine3.msf.convs.0", half128(QA), o);
+    Opt o1;
+    o1.res = QA.p;
+    o1.epi_elu = true;
+    f.conv(hB, "refine3.msf.convs.1", half128(QB), o1);
+  }
+  x2 = f.crp("refine3.crp", half128(QB), half128(QA), half128(QC), half128(QD), half128(QE));
+  Buf ref3 = f.rcu("refine3.output_convs", x2, 1, half128(QA), half128(QB), half128(QC), false, false);  // QB
+  // refine4([L1, ref3]) at full resolution
+  hA = f.rcu("refine4.adapt_convs.0", L1, 2, FA, FB, FC, false, false);            // FC
+  hB = f.rcu("refine4.adapt_convs.1", ref3, 2, half128(QA), half128(QC), half128(QD), false, false);  // QD
+  {
+    Opt o;
+    f.conv(hB, "refine4.msf.convs.1", half128(QA), o);                             // m1 (half res) -> QA
+    Opt o1;
+    o1.up = QA.p;
+    o1.epi_elu = true;
+    f.conv(hA, "refine4.msf.convs.0", FD, o1);                                     // ELU(m0 + up(m1)) -> FD
+  }
+  x2 = f.crp("refine4.crp", FD, FA, FB, FE, FC);                                   // FC
+  Buf o = f.rcu("refine4.output_convs", x2, 3, FA, FB, FD, false, true);           // FB, stats
+  // head: IN++ -> ELU -> end_conv -> / sigmas[y]
+  f.norm("normalizer", Fwd::tiles(o), 128.f, C);
+  chk(end_conv(o.p, f.ss, net->P("end_conv.weight"), net->P("end_conv.bias"), net->P("sigmas"), labels, out, B, H, W, C,
+               st),
+      "end_conv");
+}
+
+static size_t workspace_bytes(const sdp_net* net, int B) {
+  const int H = net->d.H, W = net->d.W, C = net->d.ngf, C2 = 2 * C;
+  const size_t F = (size_t)B * H * W * C, Q = (size_t)B * (H / 2) * (W / 2) * C2;
+  auto r = [](size_t n) { return ((n * 4 + 255) / 256) * 256; };
+  return r((size_t)B * (H * W / 64) * C2 * 2) + r((size_t)B * C2 * 2) + 6 * r(F) + 8 * r(Q);
+}
+
+// ------------------------------------------------------------------------------ C ABI
+static thread_local std::string g_err;
+
+int sdp_fail(const std::string& m) {
+  g_err = m;
+  return -1;
+}
+static int fail(const std::string& m) { return sdp_fail(m); }
+
+extern "C" {
+
+int sdp_version(void) { return SDP_VERSION; }
+const char* sdp_last_error(void) { return g_err.c_str(); }
+
+int sdp_net_create(const sdp_net_desc* desc, sdp_net** out) {
+  if (!desc || !out) return fail("sdp_net_create: null argument");
+  if (desc->ngf != 128 || desc->channels != 2) return fail("sdp_net_create: only ngf=128, channels=2 are built");
+  if (desc->H % 8 || desc->W % 128) return fail("sdp_net_create: H must be a multiple of 8 and W of 128");
+  if (desc->precision < 0 || desc->precision > 2) return fail("sdp_net_create: bad precision");
+  sdp_net* n = new sdp_net();
+  n->d = *desc;
+  n->mode = desc->precision;
+  *out = n;
+  return 0;
+}
+
+int sdp_net_set_param(sdp_net* net, const char* key, const float* data, const int64_t* shape, int ndim) {
+  if (!net || !key || !data || (ndim > 0 && !shape)) return fail("sdp_net_set_param: null argument");
+  HostParam hp;
+  size_t n = 1;
+  for (int i = 0; i < ndim; ++i) {
+    hp.shape.push_back(shape[i]);
+    n *= (size_t)shape[i];
+  }
+  hp.data.assign(data, data + n);
+  net->host[key] = std::move(hp);
+  net->finalized = false;
+  return 0;
+}
+
+int sdp_net_finalize(sdp_net* net) {
+  if (!net) return fail("sdp_net_finalize: null net");
+  try {
+    for (auto& kv : net->dev) chk(hipFree(kv.second), "hipFree");
+    net->dev.clear();
+    auto upload = [&](const std::string& k, const void* src, size_t bytes) {
+      void* d = nullptr;
+      chk(hipMalloc(&d, bytes), "hipMalloc");
+      chk(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice), "hipMemcpy");
+      net->dev[k] = d;
+    };
+    if (!net->host.count("sigmas")) return fail("sdp_net_finalize: missing sigmas");
+    for (auto& kv : net->host) {
+      const std::string& k = kv.first;
+      const HostParam& hp = kv.second;
+      upload(k, hp.data.data(), hp.data.size() * 4);
+      const bool is_conv_w = hp.shape.size() == 4 && k != "begin_conv.weight" && k != "end_conv.weight";
+      if (is_conv_w) {
+        if (hp.shape[0] % 32 || hp.shape[1] % 32) return fail("sdp_net_finalize: conv channels must be /32: " + k);
+        std::vector<uint32_t> fr = pack_conv_weights(hp, net->mode);
+        upload(k + "#frag", fr.data(), fr.size() * 4);
+      }
+    }
+    net->finalized = true;
+  } catch (const std::exception& e) {
+    return fail(std::string("sdp_net_finalize: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_workspace_size(const sdp_net* net, int B, size_t* bytes) {
+  if (!net || !bytes || B <= 0) return fail("sdp_net_workspace_size: bad argument");
+  *bytes = workspace_bytes(net, B);
+  return 0;
+}
+
+int sdp_net_forward(sdp_net* net, const float* x, const int64_t* labels, float* out, int B, void* ws, size_t ws_bytes,
+                    void* stream) {
+  if (!net || !x || !labels || !out || !ws || B <= 0) return fail("sdp_net_forward: bad argument");
+  if (!net->finalized) return fail("sdp_net_forward: call sdp_net_finalize first");
+  if (ws_bytes < workspace_bytes(net, B)) return fail("sdp_net_forward: workspace too small");
+  try {
+    forward_impl(net, x, labels, out, B, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream));
+  } catch (const std::exception& e) {
+    return fail(std::string("sdp_net_forward: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_profile_enable(sdp_net* net, int enable) {
+  if (!net) return fail("sdp_net_profile_enable: null net");
+  net->profile = enable != 0;
+  return 0;
+}
+
+// Synchronise on the recorded events and aggregate them per conv class.  Writes up to
+// `cap` rows of "class\tlaunches\ttotal_ms\tflops_per_launch\n" into buf (NUL-terminated)
+// and releases the events.  Returns 0; *n_launches receives the number of launches read.
+int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches) {
+  if (!net || !buf || cap == 0) return fail("sdp_net_profile_read: bad argument");
+  struct Agg { int n = 0; double ms = 0, flops = 0; };
+  std::map<std::string, Agg> agg;
+  try {
+    for (auto& r : net->prof) {
+      chk(hipEventSynchronize(r.b), "hipEventSynchronize");
+      float ms = 0.f;
+      chk(hipEventElapsedTime(&ms, r.a, r.b), "hipEventElapsedTime");
+      Agg& g = agg[r.cls];
+      g.n += 1;
+      g.ms += ms;
+      g.flops = r.flops;
+      net->ev_pool.push_back(r.a);
+      net->ev_pool.push_back(r.b);
+    }
+  } catch (const std::exception& e) {
+    return fail(std::string("sdp_net_profile_read: ") + e.what());
+  }
+  if (n_launches) *n_launches = (int)net->prof.size();
+  net->prof.clear();
+  std::string out;
+  for (auto& kv : agg)
+    out += kv.first + "\t" + std::to_string(kv.second.n) + "\t" + std::to_string(kv.second.ms) + "\t" +
+           std::to_string(kv.second.flops) + "\n";
+  std::strncpy(buf, out.c_str(), cap - 1);
+  buf[cap - 1] = 0;
+  return 0;
+}
+
+int sdp_net_destroy(sdp_net* net) {
+  delete net;
+  return 0;
+}
+
+int sdp_langevin_step(float* x, const float* grad, const float* ref, const int32_t* mask, const float* noise,
+                      uint64_t seed, uint64_t offset, float step_size, float noise_scale, float grad_ref, int nan_to_num,
+                      int B, int C, int HW, float* lik_out, uint32_t* absmax_bits, void* stream) {
+  if (!x || !grad || !ref || !mask || B <= 0 || C <= 0 || HW <= 0) return fail("sdp_langevin_step: bad argument");
+  if (HW % 4) return fail("sdp_langevin_step: H*W must be a multiple of 4");
+  hipError_t e = langevin_step(x, grad, ref, mask, noise, seed, offset, step_size, noise_scale, grad_ref, nan_to_num, B,
+                               C, HW, lik_out, absmax_bits, reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? 0 : fail(std::string("sdp_langevin_step: ") + hipGetErrorString(e));
+}
+
+int sdp_axpy_step(float* x, const float* g, float a, const float* lik, const int32_t* mask, const float* ref, float b,
+                  int n, void* stream) {
+  if (!x || n <= 0 || (g && !lik) || (!g && (!mask || !ref))) return fail("sdp_axpy_step: bad argument");
+  hipError_t e = axpy_step(x, g, a, lik, mask, ref, b, (size_t)n, reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? 0 : fail(std::string("sdp_axpy_step: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

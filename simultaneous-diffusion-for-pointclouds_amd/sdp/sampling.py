@@ -1,0 +1,201 @@
+"""Annealed-Langevin samplers with the reference's signatures, running on libsdp.
+
+  anneal_Langevin_dynamics_inpainting ....................... models/__init__.py:1385-1442
+  anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti  models/KITTISampling.py:6-513
+  anneal_Langevin_dynamics_inpainting_simultaneous_basic ....... models/__init__.py:112-602
+
+Each step is: ``scorenet(x, labels)`` (libsdp forward, or any callable returning a device
+tensor), the fused Langevin kernel (update + max|x[:,0]| for tooHigh), and -- from level
+``minStepToShare`` on -- the device consistency merge.  Host-side scalars (step size, noise
+scale, correlation ramps) are computed with the reference's numpy float32 arithmetic.
+
+Keyword-only extras (not in the reference): ``noise_fn(shape) -> cuda tensor`` injects the
+noise (parity tests); otherwise noise is Philox N(0,1) from ``seed``.  ``dist_group``
+makes tooHigh global across ranks (one 4-byte all_reduce(MAX) per merged step).
+Documented deviations: B=1 works for the kitti sampler (the reference's ``torch.squeeze``
+of the poses breaks it); the baseline keeps only the images it returns
+(it does not hold every step on the CPU, Appendix B.8) unless ``keep_all=True``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .merge import Merger, allforone_origins
+
+F32 = np.float32
+
+
+class _Stepper:
+    """Per-call device state shared by the samplers."""
+
+    def __init__(self, x_mod, refer_image, refer_mask, noise_fn, seed):
+        self.x = x_mod.detach().to(torch.float32).contiguous().clone()
+        self.dev = self.x.device
+        self.ref = refer_image.to(self.dev, torch.float32).contiguous()
+        self.mask = refer_mask.to(self.dev).to(torch.int32).contiguous()
+        self.B, self.C, self.H, self.W = self.x.shape
+        self.HW = self.H * self.W
+        self.lik = torch.empty_like(self.x)
+        self.absmax = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.noise_fn = noise_fn
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self.offset = 0
+        self._labels = {}
+
+    def labels(self, c):
+        t = self._labels.get(c)
+        if t is None:
+            t = torch.full((self.B,), int(c), dtype=torch.int64, device=self.dev)
+            self._labels[c] = t
+        return t
+
+    def step(self, grad, step_size, grad_ref, nan_to_num):
+        grad = grad.to(self.dev, torch.float32).contiguous()
+        noise = None
+        if self.noise_fn is not None:
+            noise = self.noise_fn(tuple(self.x.shape)).to(self.dev, torch.float32).contiguous()
+        nscale = F32(np.sqrt(F32(step_size * F32(2))))
+        self.absmax.zero_()
+        _lib.check(_lib.lib().sdp_langevin_step(
+            self.x.data_ptr(), grad.data_ptr(), self.ref.data_ptr(), self.mask.data_ptr(),
+            _lib.ptr(noise), self.seed, self.offset, float(step_size), float(nscale), float(grad_ref),
+            1 if nan_to_num else 0, self.B, self.C, self.HW, self.lik.data_ptr(), self.absmax.data_ptr(),
+            _lib.stream()), "langevin_step")
+        self.offset += self.x.numel() // 4
+
+    def denoise(self, grad, sigma_last, grad_ref):
+        a = F32(sigma_last) ** 2
+        grad = grad.to(self.dev, torch.float32).contiguous()
+        _lib.check(_lib.lib().sdp_axpy_step(self.x.data_ptr(), grad.data_ptr(), float(a),
+                                            self.lik.data_ptr(), None, None, float(grad_ref), self.x.numel(),
+                                            _lib.stream()), "denoise")
+
+    def final_consistency(self, grad_ref):
+        _lib.check(_lib.lib().sdp_axpy_step(self.x.data_ptr(), None, 0.0, None, self.mask.data_ptr(),
+                                            self.ref.data_ptr(), float(grad_ref), self.x.numel(), _lib.stream()),
+                   "final data consistency")
+
+    def report(self, grad_ref, c, step_size, grad):
+        d = (self.x - self.ref).abs()
+        print("grad_ref: {}, mean: {}, median: {}".format(grad_ref, d.mean(), d.median()))
+        gn = torch.norm(grad.view(self.B, -1), dim=-1).mean()
+        ln = torch.norm(self.lik.view(self.B, -1), dim=-1).mean()
+        xn = torch.norm(self.x.view(self.B, -1), dim=-1).mean()
+        print("level: {}, step_size: {}, grad_norm: {}, grad_likelihood_norm: {}, image_norm: {}".format(
+            c, step_size, gn.item(), ln.item(), xn.item()))
+
+
+def _step_size(step_lr, sigma, sigma_last):
+    """KITTISampling.py:135 in numpy float32 (python float * np.float32 stays float32)."""
+    return F32(step_lr) * (F32(sigma) / F32(sigma_last)) ** 2
+
+
+@torch.no_grad()
+def anneal_Langevin_dynamics_inpainting(x_mod, refer_image, refer_mask, scorenet, sigmas, n_steps_each=100,
+                                        step_lr=0.000008, denoise=True, verbose=True, grad_ref=0.1, sampling_step=16,
+                                        *, noise_fn=None, seed=1234, keep_all=False):
+    """Single-view baseline (models/__init__.py:1385-1442). No nan_to_num, as in the reference."""
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed)
+    sigmas = np.asarray(sigmas, dtype=np.float32)
+    images, targets = [], []
+    last = None
+    for c, sigma in enumerate(sigmas):
+        step = _step_size(step_lr, sigma, sigmas[-1])
+        for _ in range(n_steps_each):
+            grad = scorenet(S.x, S.labels(c))
+            S.step(grad, step, grad_ref, nan_to_num=False)
+            if keep_all:
+                images.append(S.x.to("cpu"))
+            last = grad
+        if verbose and c % 20 == 0:
+            S.report(grad_ref, c, step, last)
+    if not keep_all and len(sigmas) * n_steps_each > 0:
+        images.append(S.x.to("cpu"))
+    if denoise:
+        grad = scorenet(S.x, S.labels(len(sigmas) - 1))
+        S.denoise(grad, sigmas[-1], grad_ref)
+        images.append(S.x.to("cpu"))
+    S.final_consistency(grad_ref)
+    images.append(S.x.to("cpu"))
+    targets.append(refer_image.to("cpu"))
+    return images, targets
+
+
+def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr, denoise, verbose, grad_ref, cc0,
+                  merger, allowance, cc_ramp, dist_group, print_rule):
+    sigmas = np.asarray(sigmas, dtype=np.float32)
+    images, shared = [], []
+    L = len(sigmas)
+    cc = cc0
+    for c, sigma in enumerate(sigmas):
+        cc = cc_ramp(cc, c, L)
+        step = _step_size(step_lr, sigma, sigmas[-1])
+        grad = None
+        for _ in range(n_steps_each):
+            grad = scorenet(S.x, S.labels(c))
+            S.step(grad, step, grad_ref, nan_to_num=True)
+            if c >= min_step:
+                if dist_group is not None:
+                    torch.distributed.all_reduce(S.absmax, op=torch.distributed.ReduceOp.MAX, group=dist_group)
+                want = c in (0, 20, 110) or c == L - 1
+                new = torch.empty(merger.n_out, S.C, S.H, S.W, device=S.dev) if want else None
+                merger(S.x, sigma, setting, allowance, cc, S.absmax, new)
+                if c in (0, 20, 110):
+                    shared.append(new.to("cpu"))
+                if c == L - 1:
+                    images.append(new.to("cpu"))
+        if print_rule(c, verbose) and grad is not None:
+            S.report(grad_ref, c, step, grad)
+    if denoise:
+        grad = scorenet(S.x, S.labels(L - 1))
+        S.denoise(grad, sigmas[-1], grad_ref)
+    S.final_consistency(grad_ref)
+    images.append(S.x.to("cpu"))
+    return images, [], shared
+
+
+@torch.no_grad()
+def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
+        x_mod, refer_image, refer_mask, sky, x_indices, minStepToShare, setting, allowance, scorenet, sigmas, fromWorld,
+        toWorld, actualBatchSize, n_steps_each=100, step_lr=0.000008, existMask=None, denoise=True, verbose=True,
+        grad_ref=0.1, correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None):
+    """Pose-matrix simultaneous sampler (KITTISampling.py:6-513); x_indices/sampling_step unused as there."""
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed)
+    merger = Merger(S.B, actualBatchSize, S.H, S.W, S.dev, existMask, sky, S.mask, toWorld=toWorld,
+                    fromWorld=fromWorld)
+
+    def ramp(cc, c, L):  # KITTISampling.py:108-111
+        if setting == 6:
+            return 1 / (L / (c + 1))
+        if setting == 7:
+            return 0.5 / (L / (c + 1))
+        return cc
+
+    return _simultaneous(S, scorenet, sigmas, minStepToShare, setting, n_steps_each, step_lr, denoise, verbose,
+                         grad_ref, correlation_coefficient, merger, allowance, ramp, dist_group,
+                         lambda c, v: v and c % 20 == 0 or c == 1 or c == 2)  # KITTISampling.py:497 precedence
+
+
+@torch.no_grad()
+def anneal_Langevin_dynamics_inpainting_simultaneous_basic(
+        x_mod, refer_image, refer_mask, sky, x_indices, minStepToShare, setting, scorenet, sigmas, modificationList,
+        actualBatchSize, n_steps_each=100, step_lr=0.000008, existMask=None, denoise=True, verbose=True, grad_ref=0.1,
+        correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None):
+    """Origin-offset (AllForOne) simultaneous sampler (models/__init__.py:112-602)."""
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed)
+    origins = allforone_origins(modificationList)
+    merger = Merger(S.B, actualBatchSize, S.H, S.W, S.dev, existMask, sky, S.mask, origins=origins)
+    allowance = 5 if setting >= 8 else 10
+
+    def ramp(cc, c, L):  # models/__init__.py:209-212
+        if setting == 5:
+            return 1 / (L / (c + 1))
+        if setting == 6:
+            return 0.5 / (L / (c + 1))
+        return cc
+
+    return _simultaneous(S, scorenet, sigmas, minStepToShare, setting, n_steps_each, step_lr, denoise, verbose,
+                         grad_ref, correlation_coefficient, merger, allowance, ramp, dist_group,
+                         lambda c, v: v and c % 20 == 0)
