@@ -154,6 +154,9 @@ def main():
         dt = t.item()
     assert torch.isfinite(x_all).all(), "non-finite images"
     if rank == 0:
+        for k, (n_, ms_, fl_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+            print(f"[conv] {k:34s} launches {n_:5d} avg {ms_ / n_ * 1e3:8.1f} us  {fl_ / (ms_ / n_ / 1e3) / 1e12:7.1f} TF/s",
+                  file=sys.stderr)
         value = N * V * args.steps / dt
         cls, (n, ms, fl) = max(prof.items(), key=lambda kv: kv[1][1])
         avg_s = ms / n / 1e3

@@ -134,44 +134,63 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
 
 // ---------------------------------------------------------------- IN++ finalize
 // stats [B][T][C] of float2 (tile mean, tile M2) with `cnt` values per tile -> ss [B][C] of
-// float2 (scale, shift) such that IN++(x) = x*scale + shift.
-__global__ void inpp_finalize_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
-                                     const float* __restrict__ alpha, const float* __restrict__ gamma,
-                                     const float* __restrict__ beta, float2* __restrict__ ss) {
-  __shared__ double red[256];
-  const int b = blockIdx.x, c = threadIdx.x;
+// float2 (scale, shift) such that IN++(x) = x*scale + shift.  One 1024-thread block per image:
+// G = 1024/C tile groups x C channels, Chan merge of equal-count partials in float64.
+__global__ __launch_bounds__(1024) void inpp_finalize_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
+                                                             const float* __restrict__ alpha,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float2* __restrict__ ss) {
+  __shared__ double red[1024];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int G = blockDim.x / C, g = tid / C, c = tid % C;
   const float2* st = stats + (size_t)b * T * C + c;
   double sm = 0.0;
-  for (int t = 0; t < T; ++t) sm += st[(size_t)t * C].x;
-  const double mean = sm / T;
+#pragma unroll 8
+  for (int t = g; t < T; t += G) sm += st[(size_t)t * C].x;
+  red[tid] = sm;
+  __syncthreads();
+  if (g == 0) {
+    for (int k = 1; k < G; ++k) sm += red[k * C + c];
+    red[c] = sm / T;
+  }
+  __syncthreads();
+  const double mean = red[c];
+  __syncthreads();
   double m2 = 0.0;
-  for (int t = 0; t < T; ++t) {
+#pragma unroll 8
+  for (int t = g; t < T; t += G) {
     const float2 v = st[(size_t)t * C];
     const double dm = (double)v.x - mean;
     m2 += (double)v.y + dm * dm * cnt;
   }
-  const double var = m2 / ((double)T * cnt);          // biased (nn.InstanceNorm2d)
-  // m = mean_c(mean), v = unbiased var_c(mean)       (normalization.py:164-166)
-  red[c] = mean;
+  red[tid] = m2;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (c < s) red[c] += red[c + s];
+  if (g == 0)
+    for (int k = 1; k < G; ++k) m2 += red[k * C + c];
+  __syncthreads();
+  // m = mean_c(mean), v = unbiased var_c(mean)       (normalization.py:164-166)
+  if (g == 0) red[c] = mean;
+  __syncthreads();
+  for (int s = C / 2; s > 0; s >>= 1) {
+    if (g == 0 && c < s) red[c] += red[c + s];
     __syncthreads();
   }
   const double m = red[0] / C;
   __syncthreads();
-  red[c] = (mean - m) * (mean - m);
+  if (g == 0) red[c] = (mean - m) * (mean - m);
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (c < s) red[c] += red[c + s];
+  for (int s = C / 2; s > 0; s >>= 1) {
+    if (g == 0 && c < s) red[c] += red[c + s];
     __syncthreads();
   }
+  if (g != 0) return;
   const double v = red[0] / (C - 1);
+  const double var = m2 / ((double)T * cnt);          // biased (nn.InstanceNorm2d)
   const double inv = 1.0 / sqrt(var + 1e-5);
   const double mn = (mean - m) / sqrt(v + 1e-5);
-  const double g = gamma[c];
-  const double scale = g * inv;
-  const double shift = g * (-mean * inv + mn * (double)alpha[c]) + (double)beta[c];
+  const double gm = gamma[c];
+  const double scale = gm * inv;
+  const double shift = gm * (-mean * inv + mn * (double)alpha[c]) + (double)beta[c];
   ss[(size_t)b * C + c] = make_float2((float)scale, (float)shift);
 }
 
@@ -218,7 +237,7 @@ hipError_t end_conv(const float* in, const float* ss, const float* w, const floa
 
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
                          const float* beta, float* ss, hipStream_t st) {
-  hipLaunchKernelGGL(inpp_finalize_kernel, dim3(B), dim3(C), 0, st, reinterpret_cast<const float2*>(stats), T, cnt, C,
+  hipLaunchKernelGGL(inpp_finalize_kernel, dim3(B), dim3(1024), 0, st, reinterpret_cast<const float2*>(stats), T, cnt, C,
                      alpha, gamma, beta, reinterpret_cast<float2*>(ss));
   return hipGetLastError();
 }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define SDP_DEV __device__ __forceinline__
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -10,6 +12,16 @@ typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 namespace sdp {
+
+// compile-time loop: f(std::integral_constant<int, i>) for i in [B, E) -- keeps register
+// arrays indexed by literals (runtime-indexed arrays are placed in scratch by hipcc)
+template <int B, int E, class F>
+SDP_DEV void static_for(F&& f) {  // SDP_DEV = __forceinline__
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
 
 enum { MODE_F32 = 0, MODE_F32X3 = 1, MODE_BF16 = 2 };
 enum { PRO_NONE = 0, PRO_ELU = 1, PRO_AFFINE_ELU = 2 };

@@ -21,6 +21,8 @@
 //
 // Epilogue (fused): +bias, 2x2 mean-pool, +residual, +bilinear upsample of a half-res
 // tensor, ELU, a second output (value + res2), and per-tile InstanceNorm++ statistics.
+#include <type_traits>
+
 #include "common.h"
 
 namespace sdp {
@@ -34,7 +36,10 @@ struct ConvTile {
   static constexpr int PC = TC + 2 * HALO;
   static constexpr int PR = TR + 2 * HALO;
   static constexpr int NPIX = PR * PC;
-  static constexpr int LDS_BYTES = NPIX * PSTRIDE;
+  static constexpr int NU = (NPIX * 8 + 255) / 256;            // 16-B staging units per thread per chunk
+  static constexpr int PATCH_BYTES = NPIX * PSTRIDE;            // transformed (hi|lo or f32) patch
+  static constexpr int RAW_BYTES = NU * 256 * 16;               // raw fp32 patch landed by LDS-DMA
+  static constexpr int LDS_BYTES = PATCH_BYTES + RAW_BYTES;
 };
 
 SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -75,44 +80,81 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   // weight fragment pointer for (chunk, tap, nb)
-  auto wptr = [&](int chunk, int tap, int nb) -> const uint4* {
+  auto wptr = [&](int chunk, int tap, int nb) __attribute__((always_inline)) -> const uint4*  {
     return a.wf + ((size_t)((chunk * NT + tap) * NB + nbg0 + nb) * 64 + lane) * 4;
   };
-  uint4 bcur[2][4], bnext[2][4];
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) bcur[nb][q] = wptr(0, 0, nb)[q];
+  // weight fragments: ping-pong of 2 tap buffers; buffer = (tap + chunk parity) & 1 with the
+  // chunk loop unrolled by two, so every index below is a compile-time constant
+  uint4 bq[2][2][4];
+  auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
+    constexpr int J = decltype(buf)::value;
+    static_for<0, 2>([&](auto nb) {
+      static_for<0, 4>([&](auto q) { bq[J][nb][q] = wptr(chunk, tap, nb)[q]; });
+    });
+  };
+  load_b(std::integral_constant<int, 0>{}, 0, 0);
 
   const float* inb = a.in + (size_t)b * a.H * a.W * Cin;
-  const float* ssb = a.pro_ss ? a.pro_ss + (size_t)b * Cin * 2 : nullptr;
+  // scale/shift rows of this image; when there is no affine prologue point at any valid
+  // memory (loads below are unconditional, their values unused)
+  const float* ssb = a.pro_ss ? a.pro_ss + (size_t)b * Cin * 2 : a.in;
 
-  for (int chunk = 0; chunk < nchunks; ++chunk) {
-    const int c0 = chunk * 32;
-    __syncthreads();
-    // ---- stage the input patch of this 32-channel chunk into LDS (prologue applied) ----
-    for (int u = tid; u < T::NPIX * 8; u += 256) {
+  // ---- patch staging, software-pipelined: the next chunk's global loads are issued into
+  //      registers before this chunk's MFMA loop and written (prologue applied) after it ----
+  constexpr int NU = T::NU;
+  char* raw = lds + T::PATCH_BYTES;
+  float4 ssv0 = make_float4(1.f, 0.f, 1.f, 0.f), ssv1 = ssv0;   // (scale, shift) of this thread's 4 channels
+  const int my_cv = tid & 7;                                     // every unit of a thread has cv == tid % 8
+  // address of staging unit u (clamped into the image, so every load is unconditional:
+  // a load under a runtime condition makes hipcc wait vmcnt(0) right behind it) + validity
+  auto unit_src = [&](int u, int c0, bool& valid) __attribute__((always_inline)) -> int  {
+    valid = u < T::NPIX * 8;
+    u = valid ? u : 0;
+    const int pix = u >> 3, cv = u & 7;
+    const int pr = pix / T::PC, pc = pix - pr * T::PC;
+    int sr = sr0 - T::HALO + pr, sc = sc0 - T::HALO + pc;
+    if (a.circular) {
+      sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
+      sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
+    } else {
+      valid = valid && sr >= 0 && sr < Hs && sc >= 0 && sc < Ws;
+      sr = min(max(sr, 0), Hs - 1);
+      sc = min(max(sc, 0), Ws - 1);
+    }
+    const int y = sr * d + ph_r, x = sc * d + ph_c;
+    return (y * a.W + x) * Cin + c0 + cv * 4;   // < 2^31 for every shape the host admits
+  };
+  // LDS-DMA of staging unit k (no VGPR destination): lane i of a wave lands 16 B at
+  // wave base + 16*i, i.e. unit u at raw + 16*u
+  auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    if ((tid & ~63) + k * 256 >= T::NPIX * 8) return;   // whole wave past the patch (wave-uniform)
+    bool valid;
+    const float* src = inb + unit_src(tid + k * 256, chunk * 32, valid);
+    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                              reinterpret_cast<uintptr_t>(raw + ((tid & ~63) + k * 256) * 16)),
+                                     16, 0, 0);
+  };
+  auto load_ss = [&](int chunk) __attribute__((always_inline)) {
+    ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
+    ssv1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
+  };
+  auto write_patch = [&]() __attribute__((always_inline)) {
+    static_for<0, NU>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      const int u = tid + k * 256;
+      if (u >= T::NPIX * 8) return;
       const int pix = u >> 3, cv = u & 7;
-      const int pr = pix / T::PC, pc = pix - pr * T::PC;
-      int sr = sr0 - T::HALO + pr, sc = sc0 - T::HALO + pc;
-      bool valid = true;
-      if (a.circular) {
-        sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
-        sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
-      } else {
-        valid = sr >= 0 && sr < Hs && sc >= 0 && sc < Ws;
-      }
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 v = *reinterpret_cast<const float4*>(raw + u * 16);
+      bool valid;
+      (void)unit_src(u, 0, valid);
+      if (!valid) v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid) {
-        const int y = sr * d + ph_r, x = sc * d + ph_c;
-        const int c = c0 + cv * 4;
-        v = ld4(inb + ((size_t)y * a.W + x) * Cin + c);
         if (a.pro_mode == PRO_AFFINE_ELU) {
-          const float4 s01 = ld4(ssb + c * 2), s23 = ld4(ssb + c * 2 + 4);
-          v.x = elu(fmaf(v.x, s01.x, s01.y));
-          v.y = elu(fmaf(v.y, s01.z, s01.w));
-          v.z = elu(fmaf(v.z, s23.x, s23.y));
-          v.w = elu(fmaf(v.w, s23.z, s23.w));
+          v.x = elu(fmaf(v.x, ssv0.x, ssv0.y));
+          v.y = elu(fmaf(v.y, ssv0.z, ssv0.w));
+          v.z = elu(fmaf(v.z, ssv1.x, ssv1.y));
+          v.w = elu(fmaf(v.w, ssv1.z, ssv1.w));
         } else if (a.pro_mode == PRO_ELU) {
           v.x = elu(v.x); v.y = elu(v.y); v.z = elu(v.z); v.w = elu(v.w);
         }
@@ -132,24 +174,32 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
           *reinterpret_cast<bf16x4*>(dst + 64 + cv * 8) = lo;
         }
       }
-    }
-    __syncthreads();
+    });
+  };
 
-    // ---- 9 (or 1) taps over the staged patch ----
-#pragma unroll 1
-    for (int tap = 0; tap < NT; ++tap) {
-      // prefetch next tap's weight fragments (or next chunk's first tap)
-      {
-        int ntap = tap + 1, nchunk = chunk;
-        if (ntap == NT) { ntap = 0; ++nchunk; }
-        if (nchunk < nchunks) {
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bnext[nb][q] = wptr(nchunk, ntap, nb)[q];
-        }
+  load_ss(0);
+  static_for<0, NU>([&](auto k) { load_unit(k, 0); });
+  auto do_chunk = [&](auto parity, int chunk) __attribute__((always_inline)) {
+    constexpr int P = decltype(parity)::value;
+    __syncthreads();
+    write_patch();
+    __syncthreads();
+    const bool more = chunk + 1 < nchunks;
+
+    // ---- 9 (or 1) taps over the staged patch; per tap: prefetch the next tap's weight
+    //      fragments, issue a slice of the next chunk's patch loads, then the MFMAs ----
+    static_for<0, NT>([&](auto tap_c) {
+      constexpr int tap = decltype(tap_c)::value;
+      constexpr int CUR = (tap + P) & 1, NXT = (tap + 1 + P) & 1;
+      if constexpr (tap + 1 < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + 1);
+      else if (more) load_b(std::integral_constant<int, NXT>{}, chunk + 1, 0);
+      if (more) {
+        if constexpr (tap == 0) load_ss(chunk + 1);
+        static_for<0, NU>([&](auto kc) {
+          if constexpr (decltype(kc)::value % NT == tap) load_unit(kc, chunk + 1);
+        });
       }
-      const int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap - (tap / 3) * 3 : 0;
+      const int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
       if constexpr (MODE == MODE_F32) {
         float av[2][16];
 #pragma unroll
@@ -166,8 +216,8 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
         for (int k = 0; k < 16; ++k) {
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb) {
-            const uint4 bq = bcur[nb][k >> 2];
-            const uint32_t bw = (k & 3) == 0 ? bq.x : (k & 3) == 1 ? bq.y : (k & 3) == 2 ? bq.z : bq.w;
+            const uint4 bv = bq[CUR][nb][k >> 2];
+            const uint32_t bw = (k & 3) == 0 ? bv.x : (k & 3) == 1 ? bv.y : (k & 3) == 2 ? bv.z : bv.w;
             const float bf = __uint_as_float(bw);
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb)
@@ -187,7 +237,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
           }
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb) {
-            const uint4 h4 = bcur[nb][2 * s], l4 = bcur[nb][2 * s + 1];
+            const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
             const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
             const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
 #pragma unroll
@@ -201,11 +251,12 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
           }
         }
       }
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bcur[nb][q] = bnext[nb][q];
-    }
+    });
+  };
+  static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
+  for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
+    do_chunk(std::integral_constant<int, 0>{}, chunk);
+    do_chunk(std::integral_constant<int, 1>{}, chunk + 1);
   }
 
   // ------------------------------------------------------------------ epilogue
@@ -308,7 +359,7 @@ static hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
 
 template <int MODE>
 static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int tc, hipStream_t st) {
-  if (ks == 1) return pool ? launch_t<MODE, 64, 1, true>(a, st) : launch_t<MODE, 64, 1, false>(a, st);
+  if (ks == 1) return launch_t<MODE, 64, 1, true>(a, st);   // only the ConvMeanPool 1x1 shortcut
   if (pool) return tc == 64 ? launch_t<MODE, 64, 3, true>(a, st) : launch_t<MODE, 32, 3, true>(a, st);
   return tc == 64 ? launch_t<MODE, 64, 3, false>(a, st) : launch_t<MODE, 32, 3, false>(a, st);
 }
@@ -316,13 +367,14 @@ static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int tc, hipS
 // Host entry: validates the shape contract the kernel's indexing assumes, then launches.
 hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, const char** why) {
   const int d = a.dil;
-  if (a.Cin % 32 || a.Cout % 128) { *why = "conv: Cin%32 and Cout%128 required"; return hipErrorInvalidValue; }
+  if (a.Cin % 64 || a.Cout % 128) { *why = "conv: Cin%64 and Cout%128 required"; return hipErrorInvalidValue; }
   if (a.H % d || a.W % d) { *why = "conv: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
   const int Hs = a.H / d, Ws = a.W / d;
   int tc = (Ws % 64 == 0) ? 64 : 32;
   if (ks == 1) tc = 64;
   const int tr = 128 / tc;
   if (Ws % tc || Hs % tr) { *why = "conv: sub-grid not divisible by the 128-pixel tile"; return hipErrorInvalidValue; }
+  if (ks == 1 && !pool) { *why = "conv: 1x1 only as the pooled shortcut"; return hipErrorInvalidValue; }
   if (pool && (d != 1 || (a.H & 1) || (a.W & 1))) { *why = "conv: pooling needs d=1, even H,W"; return hipErrorInvalidValue; }
   if (a.up && ((a.H & 1) || (a.W & 1) || a.H < 2 || a.W < 2)) { *why = "conv: upsample needs even H,W"; return hipErrorInvalidValue; }
   if (!a.circular && d != 1) { *why = "conv: zero padding only for d=1"; return hipErrorInvalidValue; }

@@ -12,6 +12,9 @@
 // denoise step (KITTISampling.py:505 uses the last loop step's grad_likelihood).
 #include "common.h"
 
+// reference evaluation order: no FMA contraction in this file (HIP __fmul_rn is a plain `*`)
+#pragma clang fp contract(off)
+
 namespace sdp {
 
 struct Philox {

@@ -15,6 +15,9 @@
 // reference's unstable argsort leaves it unspecified).
 #include "merge.h"
 
+// reference evaluation order: no FMA contraction in this file (HIP __fmul_rn is a plain `*`)
+#pragma clang fp contract(off)
+
 namespace sdp {
 
 // ---------------------------------------------------------------- K0: source points -> world

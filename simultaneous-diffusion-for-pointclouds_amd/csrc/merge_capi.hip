@@ -7,6 +7,9 @@
 
 int sdp_fail(const std::string& m);
 
+// reference evaluation order: no FMA contraction in this file (HIP __fmul_rn is a plain `*`)
+#pragma clang fp contract(off)
+
 namespace sdp {
 
 static long floordiv(long a, long b) {  // Python // on ints

@@ -20,7 +20,7 @@ run() {  # name timeout cmd...
 }
 STEPS=${STEPS:-all}
 [[ $STEPS == *smoke* || $STEPS == all ]] && run smoke 400 python __graft_entry__.py smoke
-[[ $STEPS == *tests* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q -rA -x
+[[ $STEPS == *tests* || $STEPS == all ]] && run pytest_gpu 900 python -m pytest tests -m gpu -q -rA
 [[ $STEPS == *bench* || $STEPS == all ]] && run bench 600 python bench.py --steps 20 --warmup 3
 [[ $STEPS == *prof* || $STEPS == all ]] && run rocprof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline
 exit 0
