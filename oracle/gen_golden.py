@@ -244,7 +244,9 @@ def gen_kitti_e2e():
                             torch.from_numpy(case["toWorld"].reshape(B, 1, 4, 4)), B,
                             n_steps_each=2, step_lr=6.2e-6, existMask=torch.from_numpy(case["exist"]),
                             denoise=True, verbose=False, grad_ref=1, correlation_coefficient=0.01)
-    save("kitti_e2e_b2_64x256.npz", new=imgs[0].numpy(), final=imgs[1].numpy())
+    # images = [newImages (last level, step 1), newImages (step 2), final x]  (KITTISampling.py:418-419, 511)
+    assert len(imgs) == 3
+    save("kitti_e2e_b2_64x256.npz", new=imgs[0].numpy(), new2=imgs[1].numpy(), final=imgs[2].numpy())
 
 
 def gen_dsm():

@@ -46,6 +46,7 @@ SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p);
 
 template <int MODE, int TC, int KS, bool POOL>
 __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
   using T = ConvTile<TC, KS>;
   constexpr int NT = KS * KS;
   __shared__ __attribute__((aligned(16))) char lds[T::LDS_BYTES];
@@ -79,17 +80,20 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // weight fragment pointer for (chunk, tap, nb)
-  auto wptr = [&](int chunk, int tap, int nb) __attribute__((always_inline)) -> const uint4*  {
-    return a.wf + ((size_t)((chunk * NT + tap) * NB + nbg0 + nb) * 64 + lane) * 4;
-  };
-  // weight fragments: ping-pong of 2 tap buffers; buffer = (tap + chunk parity) & 1 with the
-  // chunk loop unrolled by two, so every index below is a compile-time constant
+  // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
+  // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wf, 0, 0x7fffffff, 0x00020000);
+  const int wv0 = ((nbg0 + 0) * 64 + lane) * 64, wv1 = ((nbg0 + 1) * 64 + lane) * 64;
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
   uint4 bq[2][2][4];
   auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
     constexpr int J = decltype(buf)::value;
-    static_for<0, 2>([&](auto nb) {
-      static_for<0, 4>([&](auto q) { bq[J][nb][q] = wptr(chunk, tap, nb)[q]; });
+    const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096);
+    static_for<0, 4>([&](auto q) {
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
+      bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+      bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
     });
   };
   load_b(std::integral_constant<int, 0>{}, 0, 0);
@@ -105,10 +109,17 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   char* raw = lds + T::PATCH_BYTES;
   float4 ssv0 = make_float4(1.f, 0.f, 1.f, 0.f), ssv1 = ssv0;   // (scale, shift) of this thread's 4 channels
   const int my_cv = tid & 7;                                     // every unit of a thread has cv == tid % 8
-  // address of staging unit u (clamped into the image, so every load is unconditional:
-  // a load under a runtime condition makes hipcc wait vmcnt(0) right behind it) + validity
-  auto unit_src = [&](int u, int c0, bool& valid) __attribute__((always_inline)) -> int  {
-    valid = u < T::NPIX * 8;
+  // Staging unit u = 16 B (4 channels) of one patch pixel.  Its byte offset inside the image
+  // (clamped into range, so every load is unconditional) and its validity (zero padding)
+  // depend only on the tile, so they are computed once; per chunk only the scalar channel
+  // offset changes.
+  const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, 0x7fffffff, 0x00020000);
+  int uoff[NU];
+  unsigned uvalid = 0;
+  static_for<0, NU>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    int u = tid + k * 256;
+    bool valid = u < T::NPIX * 8;
     u = valid ? u : 0;
     const int pix = u >> 3, cv = u & 7;
     const int pr = pix / T::PC, pc = pix - pr * T::PC;
@@ -122,18 +133,18 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       sc = min(max(sc, 0), Ws - 1);
     }
     const int y = sr * d + ph_r, x = sc * d + ph_c;
-    return (y * a.W + x) * Cin + c0 + cv * 4;   // < 2^31 for every shape the host admits
-  };
-  // LDS-DMA of staging unit k (no VGPR destination): lane i of a wave lands 16 B at
-  // wave base + 16*i, i.e. unit u at raw + 16*u
+    uoff[k] = ((y * a.W + x) * Cin + cv * 4) * 4;   // bytes, < 2^31 for every admitted shape
+    uvalid |= (valid ? 1u : 0u) << k;
+  });
+  // LDS-DMA of staging unit k (no VGPR destination): lane i of a wave lands 16 B at the
+  // wave-uniform base + 16*i, i.e. unit u at raw + 16*u
   auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     if ((tid & ~63) + k * 256 >= T::NPIX * 8) return;   // whole wave past the patch (wave-uniform)
-    bool valid;
-    const float* src = inb + unit_src(tid + k * 256, chunk * 32, valid);
-    __builtin_amdgcn_global_load_lds(src, reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                              reinterpret_cast<uintptr_t>(raw + ((tid & ~63) + k * 256) * 16)),
-                                     16, 0, 0);
+    const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
+        uoff[k], chunk * 128, 0, 0);
   };
   auto load_ss = [&](int chunk) __attribute__((always_inline)) {
     ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
@@ -146,8 +157,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       if (u >= T::NPIX * 8) return;
       const int pix = u >> 3, cv = u & 7;
       float4 v = *reinterpret_cast<const float4*>(raw + u * 16);
-      bool valid;
-      (void)unit_src(u, 0, valid);
+      const bool valid = (uvalid >> k) & 1u;
       if (!valid) v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (valid) {
         if (a.pro_mode == PRO_AFFINE_ELU) {
@@ -199,6 +209,9 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
           if constexpr (decltype(kc)::value % NT == tap) load_unit(kc, chunk + 1);
         });
       }
+      // keep the prefetches ahead of this tap's MFMAs (hipcc otherwise sinks them to the end
+      // of the tap, exposing their latency at the next tap)
+      __builtin_amdgcn_sched_barrier(0);
       const int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
       if constexpr (MODE == MODE_F32) {
         float av[2][16];
@@ -347,6 +360,7 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       }
     }
   }
+#endif
 }
 
 // ----------------------------------------------------------------------------- launch

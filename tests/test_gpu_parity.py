@@ -212,5 +212,5 @@ def test_kitti_sampler_end_to_end_matches_golden(net256):
                         existMask=t(case["exist"]), denoise=True, verbose=False, grad_ref=1,
                         correlation_coefficient=0.01, noise_fn=_noise_feed("e2e"))
     assert len(images) == 3
-    for got, want in ((images[0].numpy(), f["new"]), (images[-1].numpy(), f["final"])):
+    for got, want in ((images[0].numpy(), f["new"]), (images[1].numpy(), f["new2"]), (images[2].numpy(), f["final"])):
         assert _close_frac(got, want, rtol=1e-4, atol=1e-4 * np.abs(want).max()) <= 1e-3

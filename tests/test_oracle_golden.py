@@ -166,5 +166,7 @@ def test_kitti_sampler_end_to_end(params128):
     images, _, _ = S.sampler_kitti(x0, case["ref"], case["mask"], case["sky"], 2, 5, 10, _score_fn(params128),
                                    get_sigmas_np()[229:232], case["fromWorld"], case["toWorld"], 2, 2, 6.2e-6,
                                    case["exist"], _noise_feed("e2e"))
+    assert len(images) == 3
     np.testing.assert_allclose(images[0], f["new"], rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(images[1], f["final"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(images[1], f["new2"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(images[2], f["final"], rtol=1e-5, atol=1e-5)
