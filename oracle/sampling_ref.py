@@ -135,17 +135,20 @@ def _apply(x, new, maskimg, sky, refmask, too_high, cc):
     return (x + F32(cc) * corr).astype(np.float32)
 
 
-def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5, allowance=10, cc=0.01):
+def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5, allowance=10, cc=0.01,
+                absmax=None):
     """One consistency merge of the pose-matrix sampler (KITTISampling.py:160-490).
 
     x f32 [B,2,H,W] (after the Langevin update); returns (newImages f32, x corrected f32).
+    absmax: max|x[:,0]| over every view of the step when x holds only some of them.
     """
     B, _, H, W = x.shape
     g = merge_geometry(H, W)
     smod = sigma_mod_of(sigma)
     x0 = x[:, 0]
     isneg = x0 < 0
-    too_high = bool(F32(F32(np.abs(x0).max()) * F32(6)) / F32(smod) > 50)
+    m = F32(np.abs(x0).max()) if absmax is None else F32(absmax)
+    too_high = bool(F32(m * F32(6)) / F32(smod) > 50)
     rd = real_distance(x0, smod).astype(np.float64)
     caz, saz = np.cos(g["az"])[None, None, :], np.sin(g["az"])[None, None, :]
     cel, sel = np.cos(g["el"])[None, :, None], np.sin(g["el"])[None, :, None]

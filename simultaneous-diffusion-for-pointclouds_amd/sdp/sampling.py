@@ -9,9 +9,12 @@ tensor), the fused Langevin kernel (update + max|x[:,0]| for tooHigh), and -- fr
 ``minStepToShare`` on -- the device consistency merge.  Host-side scalars (step size, noise
 scale, correlation ramps) are computed with the reference's numpy float32 arithmetic.
 
-Keyword-only extras (not in the reference): ``noise_fn(shape) -> cuda tensor`` injects the
-noise (parity tests); otherwise noise is Philox N(0,1) from ``seed``.  ``dist_group``
-makes tooHigh global across ranks (one 4-byte all_reduce(MAX) per merged step).
+Keyword-only extras (not in the reference): ``noise_fn(shape) -> tensor`` injects the
+noise (parity tests); otherwise noise is Philox N(0,1) from ``seed``.  ``dist_group`` makes
+tooHigh global across ranks (one 4-byte all_reduce(MAX) per merged step); with
+``view_shard=(rank, world)`` the call's views are one megabatch split across ranks: each
+rank passes only its own views, the megabatch images are all-gathered every merged step
+(the cross-view consistency gather) and each rank merges into its own views.
 Documented deviations: B=1 works for the kitti sampler (the reference's ``torch.squeeze``
 of the poses breaks it); the baseline keeps only the images it returns
 (it does not hold every step on the CPU, Appendix B.8) unless ``keep_all=True``.
@@ -21,21 +24,47 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from . import _lib
 from .merge import Merger, allforone_origins
 
 F32 = np.float32
 
 
-class _Stepper:
-    """Per-call device state shared by the samplers."""
+class DeviceOps:
+    """The device operations of a step, on libsdp (one HIP stream: torch's current)."""
 
-    def __init__(self, x_mod, refer_image, refer_mask, noise_fn, seed):
-        self.x = x_mod.detach().to(torch.float32).contiguous().clone()
-        self.dev = self.x.device
+    def langevin(self, x, grad, ref, mask, noise, seed, offset, step, nscale, grad_ref, nan_to_num, lik, absmax):
+        from . import _lib
+        B, C, H, W = x.shape
+        _lib.check(_lib.lib().sdp_langevin_step(
+            x.data_ptr(), grad.data_ptr(), ref.data_ptr(), mask.data_ptr(), _lib.ptr(noise), seed, offset,
+            float(step), float(nscale), float(grad_ref), 1 if nan_to_num else 0, B, C, H * W, lik.data_ptr(),
+            absmax.data_ptr(), _lib.stream()), "langevin_step")
+
+    def axpy(self, x, g, a, lik, mask, ref, b):
+        from . import _lib
+        _lib.check(_lib.lib().sdp_axpy_step(x.data_ptr(), _lib.ptr(g), float(a), _lib.ptr(lik), _lib.ptr(mask),
+                                            _lib.ptr(ref), float(b), x.numel(), _lib.stream()), "axpy")
+
+    def make_merger(self, *args, **kw):
+        return Merger(*args, **kw)
+
+
+class _Stepper:
+    """Per-call state shared by the samplers.  ``x`` is this rank's views; with a view shard
+    it is a contiguous slice of ``x_all`` (the whole megabatch)."""
+
+    def __init__(self, x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all=None, own0=0):
+        self.ops = ops
+        x = x_mod.detach().to(torch.float32).contiguous()
+        self.B, self.C, self.H, self.W = x.shape
+        self.dev = x.device
+        n_all = self.B if n_all is None else n_all
+        self.x_all = torch.zeros((n_all, self.C, self.H, self.W), dtype=torch.float32, device=self.dev)
+        self.own0 = own0
+        self.x = self.x_all[own0:own0 + self.B]
+        self.x.copy_(x)
         self.ref = refer_image.to(self.dev, torch.float32).contiguous()
         self.mask = refer_mask.to(self.dev).to(torch.int32).contiguous()
-        self.B, self.C, self.H, self.W = self.x.shape
         self.HW = self.H * self.W
         self.lik = torch.empty_like(self.x)
         self.absmax = torch.zeros(1, dtype=torch.int32, device=self.dev)
@@ -58,31 +87,23 @@ class _Stepper:
             noise = self.noise_fn(tuple(self.x.shape)).to(self.dev, torch.float32).contiguous()
         nscale = F32(np.sqrt(F32(step_size * F32(2))))
         self.absmax.zero_()
-        _lib.check(_lib.lib().sdp_langevin_step(
-            self.x.data_ptr(), grad.data_ptr(), self.ref.data_ptr(), self.mask.data_ptr(),
-            _lib.ptr(noise), self.seed, self.offset, float(step_size), float(nscale), float(grad_ref),
-            1 if nan_to_num else 0, self.B, self.C, self.HW, self.lik.data_ptr(), self.absmax.data_ptr(),
-            _lib.stream()), "langevin_step")
+        self.ops.langevin(self.x, grad, self.ref, self.mask, noise, self.seed, self.offset, step_size, nscale,
+                          grad_ref, nan_to_num, self.lik, self.absmax)
         self.offset += self.x.numel() // 4
 
     def denoise(self, grad, sigma_last, grad_ref):
-        a = F32(sigma_last) ** 2
         grad = grad.to(self.dev, torch.float32).contiguous()
-        _lib.check(_lib.lib().sdp_axpy_step(self.x.data_ptr(), grad.data_ptr(), float(a),
-                                            self.lik.data_ptr(), None, None, float(grad_ref), self.x.numel(),
-                                            _lib.stream()), "denoise")
+        self.ops.axpy(self.x, grad, F32(sigma_last) ** 2, self.lik, None, None, grad_ref)
 
     def final_consistency(self, grad_ref):
-        _lib.check(_lib.lib().sdp_axpy_step(self.x.data_ptr(), None, 0.0, None, self.mask.data_ptr(),
-                                            self.ref.data_ptr(), float(grad_ref), self.x.numel(), _lib.stream()),
-                   "final data consistency")
+        self.ops.axpy(self.x, None, 0.0, None, self.mask, self.ref, grad_ref)
 
     def report(self, grad_ref, c, step_size, grad):
         d = (self.x - self.ref).abs()
         print("grad_ref: {}, mean: {}, median: {}".format(grad_ref, d.mean(), d.median()))
-        gn = torch.norm(grad.view(self.B, -1), dim=-1).mean()
-        ln = torch.norm(self.lik.view(self.B, -1), dim=-1).mean()
-        xn = torch.norm(self.x.view(self.B, -1), dim=-1).mean()
+        gn = torch.norm(grad.reshape(self.B, -1), dim=-1).mean()
+        ln = torch.norm(self.lik.reshape(self.B, -1), dim=-1).mean()
+        xn = torch.norm(self.x.reshape(self.B, -1), dim=-1).mean()
         print("level: {}, step_size: {}, grad_norm: {}, grad_likelihood_norm: {}, image_norm: {}".format(
             c, step_size, gn.item(), ln.item(), xn.item()))
 
@@ -95,9 +116,9 @@ def _step_size(step_lr, sigma, sigma_last):
 @torch.no_grad()
 def anneal_Langevin_dynamics_inpainting(x_mod, refer_image, refer_mask, scorenet, sigmas, n_steps_each=100,
                                         step_lr=0.000008, denoise=True, verbose=True, grad_ref=0.1, sampling_step=16,
-                                        *, noise_fn=None, seed=1234, keep_all=False):
+                                        *, noise_fn=None, seed=1234, keep_all=False, ops=None):
     """Single-view baseline (models/__init__.py:1385-1442). No nan_to_num, as in the reference."""
-    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed)
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops or DeviceOps())
     sigmas = np.asarray(sigmas, dtype=np.float32)
     images, targets = [], []
     last = None
@@ -123,8 +144,18 @@ def anneal_Langevin_dynamics_inpainting(x_mod, refer_image, refer_mask, scorenet
     return images, targets
 
 
+def _gather_views(S, group):
+    """All-gather this rank's views into the megabatch buffer (RCCL over xGMI on GPUs)."""
+    dist = torch.distributed
+    if S.x_all.is_cuda:
+        dist.all_gather_into_tensor(S.x_all, S.x, group=group)
+    else:  # gloo: list form
+        parts = list(S.x_all.chunk(S.x_all.shape[0] // S.B))
+        dist.all_gather(parts, S.x.clone(), group=group)
+
+
 def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr, denoise, verbose, grad_ref, cc0,
-                  merger, allowance, cc_ramp, dist_group, print_rule):
+                  merger, allowance, cc_ramp, dist_group, view_split, print_rule):
     sigmas = np.asarray(sigmas, dtype=np.float32)
     images, shared = [], []
     L = len(sigmas)
@@ -137,11 +168,13 @@ def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr,
             grad = scorenet(S.x, S.labels(c))
             S.step(grad, step, grad_ref, nan_to_num=True)
             if c >= min_step:
-                if dist_group is not None:
+                if view_split:
+                    _gather_views(S, dist_group)
+                if dist_group is not None or (view_split and torch.distributed.is_initialized()):
                     torch.distributed.all_reduce(S.absmax, op=torch.distributed.ReduceOp.MAX, group=dist_group)
                 want = c in (0, 20, 110) or c == L - 1
                 new = torch.empty(merger.n_out, S.C, S.H, S.W, device=S.dev) if want else None
-                merger(S.x, sigma, setting, allowance, cc, S.absmax, new)
+                merger(S.x_all, sigma, setting, allowance, cc, S.absmax, new)
                 if c in (0, 20, 110):
                     shared.append(new.to("cpu"))
                 if c == L - 1:
@@ -156,15 +189,35 @@ def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr,
     return images, [], shared
 
 
+def _shard_setup(x_mod, actualBatchSize, view_shard):
+    """(n_all, own0): the views this call's buffers hold and where this rank's start."""
+    B = x_mod.shape[0]
+    if view_shard is None:
+        return B, 0
+    rank, world = view_shard
+    if B * world != actualBatchSize:
+        raise ValueError("view_shard: each rank must hold actualBatchSize / world views of ONE megabatch")
+    return B * world, rank * B
+
+
 @torch.no_grad()
 def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
         x_mod, refer_image, refer_mask, sky, x_indices, minStepToShare, setting, allowance, scorenet, sigmas, fromWorld,
         toWorld, actualBatchSize, n_steps_each=100, step_lr=0.000008, existMask=None, denoise=True, verbose=True,
-        grad_ref=0.1, correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None):
-    """Pose-matrix simultaneous sampler (KITTISampling.py:6-513); x_indices/sampling_step unused as there."""
-    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed)
-    merger = Merger(S.B, actualBatchSize, S.H, S.W, S.dev, existMask, sky, S.mask, toWorld=toWorld,
-                    fromWorld=fromWorld)
+        grad_ref=0.1, correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None,
+        view_shard=None, all_refer_mask=None, all_sky=None, ops=None):
+    """Pose-matrix simultaneous sampler (KITTISampling.py:6-513); x_indices/sampling_step unused as there.
+
+    With ``view_shard=(rank, world)``: x_mod/refer_* hold this rank's views, while fromWorld,
+    toWorld, ``all_sky`` and ``all_refer_mask`` describe every view of the megabatch.
+    """
+    ops = ops or DeviceOps()
+    n_all, own0 = _shard_setup(x_mod, actualBatchSize, view_shard)
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0)
+    sky_all = sky if view_shard is None else all_sky
+    mask_all = S.mask if view_shard is None else all_refer_mask
+    merger = ops.make_merger(n_all, actualBatchSize, S.H, S.W, S.dev, existMask, sky_all, mask_all, toWorld=toWorld,
+                             fromWorld=fromWorld, o_begin=own0, n_out=S.B)
 
     def ramp(cc, c, L):  # KITTISampling.py:108-111
         if setting == 6:
@@ -174,7 +227,7 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
         return cc
 
     return _simultaneous(S, scorenet, sigmas, minStepToShare, setting, n_steps_each, step_lr, denoise, verbose,
-                         grad_ref, correlation_coefficient, merger, allowance, ramp, dist_group,
+                         grad_ref, correlation_coefficient, merger, allowance, ramp, dist_group, view_shard is not None,
                          lambda c, v: v and c % 20 == 0 or c == 1 or c == 2)  # KITTISampling.py:497 precedence
 
 
@@ -182,11 +235,17 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
 def anneal_Langevin_dynamics_inpainting_simultaneous_basic(
         x_mod, refer_image, refer_mask, sky, x_indices, minStepToShare, setting, scorenet, sigmas, modificationList,
         actualBatchSize, n_steps_each=100, step_lr=0.000008, existMask=None, denoise=True, verbose=True, grad_ref=0.1,
-        correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None):
+        correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None, view_shard=None,
+        all_refer_mask=None, all_sky=None, ops=None):
     """Origin-offset (AllForOne) simultaneous sampler (models/__init__.py:112-602)."""
-    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed)
+    ops = ops or DeviceOps()
+    n_all, own0 = _shard_setup(x_mod, actualBatchSize, view_shard)
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0)
+    sky_all = sky if view_shard is None else all_sky
+    mask_all = S.mask if view_shard is None else all_refer_mask
     origins = allforone_origins(modificationList)
-    merger = Merger(S.B, actualBatchSize, S.H, S.W, S.dev, existMask, sky, S.mask, origins=origins)
+    merger = ops.make_merger(n_all, actualBatchSize, S.H, S.W, S.dev, existMask, sky_all, mask_all, origins=origins,
+                             o_begin=own0, n_out=S.B)
     allowance = 5 if setting >= 8 else 10
 
     def ramp(cc, c, L):  # models/__init__.py:209-212
@@ -197,5 +256,5 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic(
         return cc
 
     return _simultaneous(S, scorenet, sigmas, minStepToShare, setting, n_steps_each, step_lr, denoise, verbose,
-                         grad_ref, correlation_coefficient, merger, allowance, ramp, dist_group,
+                         grad_ref, correlation_coefficient, merger, allowance, ramp, dist_group, view_shard is not None,
                          lambda c, v: v and c % 20 == 0)
