@@ -28,6 +28,9 @@ enum { PRO_NONE = 0, PRO_ELU = 1, PRO_AFFINE_ELU = 2 };
 
 // nn.ELU(alpha=1) (LiDARGen/models/layers.py:11-13)
 SDP_DEV float elu(float x) { return x > 0.f ? x : (__expf(x) - 1.0f); }
+// the same values without a compare/select (e^x - 1 >= x, and e^min(x,0) - 1 = 0 for x > 0):
+// no VCC round trip, so it schedules freely between MFMAs
+SDP_DEV float elu_max(float x) { return fmaxf(x, __expf(fminf(x, 0.f)) - 1.0f); }
 
 // Arguments of one implicit-GEMM 3x3 / 1x1 convolution launch (activations NHWC float32).
 struct ConvArgs {
@@ -40,10 +43,11 @@ struct ConvArgs {
   const float* res2;
   const float* up;         // [B][H/2][W/2][Cout]: bilinear(align_corners) upsample-add, or null
   const float* pro_ss;     // [B][Cin][2] (scale, shift) for PRO_AFFINE_ELU
-  float* stats;            // [B][tiles_per_img][Cout][2] per-tile (mean, M2) or null
+  float* stats;            // [B][groups_per_img][Cout][2] per-128-pixel (mean, M2) or null
   int B, H, W, Cin, Cout;
   int dil, circular, pro_mode, epi_elu;
-  int tiles_per_img;
+  int tiles_per_img;       // workgroup tiles per image (set by the launcher)
+  int groups_per_img;      // 128-pixel statistics groups per image (H*W/128)
 };
 
 }  // namespace sdp

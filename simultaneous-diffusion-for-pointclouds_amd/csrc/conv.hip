@@ -4,23 +4,33 @@
 //   conv3x3 circular (LiDARGen/models/layers.py:37-44), dilated_conv3x3 circular
 //   (layers.py:55-60), ConvMeanPool 3x3/1x1 zero-pad + 2x2 mean (layers.py:291-313).
 //
-// GEMM view: M = output pixels, N = Cout, K = taps x Cin.  One 256-thread workgroup owns
-// a 128-pixel x 128-channel output tile; 4 waves each own 64 px x 64 ch = 2x2 blocks of a
-// 32x32 MFMA tile.  Dilated convs are run on their d x d polyphase sub-grids, so a tile is
-// always TR x TC pixels of one sub-grid and its input patch has a 1-pixel halo whatever d.
-// Per 32-channel chunk the (TR+2)x(TC+2) input patch is staged once into LDS -- with the
-// consumer-side prologue (ELU or InstanceNorm++ affine + ELU) applied on the way -- and
-// reused by all 9 taps.  Weights are pre-arranged on the host in MFMA fragment order and
-// streamed from L2 straight into VGPRs (one tap ahead).
+// GEMM view: M = output pixels, N = Cout, K = taps x Cin.  One workgroup = 4 waves, ONE wave
+// per SIMD (512-register budget, accumulators in AGPRs); each wave owns 128 px x 64 Cout =
+// 4 x 2 blocks of the 32x32 MFMA tile, so per (tap, 16-wide k step) it reads 8 A fragments
+// from LDS and 4 B fragments from L2 for 24 MFMAs (fp32x3).  Workgroup shapes:
+//   WM=1: 128 px x 256 Cout (4 waves side by side in N; the patch serves 256 channels)
+//   WM=2: 256 px x 128 Cout (2 x 2 waves; for the 128-channel layers)
+// Dilated convs run on their d x d polyphase sub-grids, so a tile is always TR x TC pixels
+// of one sub-grid and its input patch has a 1-pixel halo whatever d.
+//
+// K loop, per 32-channel chunk, fully software-pipelined (one barrier per chunk):
+//   raw   : the fp32 (TR+2) x (TC+2) x 32 input patch of chunk k+1, landed by LDS-DMA
+//           (buffer_load ... lds) during chunk k-1
+//   patch : two buffers; while the 9 taps of chunk k run their MFMAs on patch[k&1], the
+//           taps 0..3 transform raw -> patch[(k+1)&1] (consumer prologue: InstanceNorm++
+//           affine and/or ELU, zero padding, bf16 hi/lo split) and the taps 4..8 issue the
+//           LDS-DMA of chunk k+2 into raw.
+//   weights: pre-arranged on the host in MFMA fragment order, streamed from L2 into VGPRs
+//           one tap ahead (buffer_load_b128 with a scalar per-(chunk, tap) offset).
 //
 // MODE_F32   : v_mfma_f32_32x32x2_f32 on fp32 operands (exact fp32 products).
 // MODE_F32X3 : operands split x = hi + lo (bf16 each), acc += hi*hi + hi*lo + lo*hi on
-//              v_mfma_f32_32x32x16_bf16 -- error ~2e-5 of max|out| on the full network
-//              (fp32 alone ~2e-6), 16x the issue rate of the fp32 MFMA per pass.
+//              v_mfma_f32_32x32x16_bf16 -- error ~2e-5 of max|out| on the full network.
 // MODE_BF16  : hi*hi only.
 //
 // Epilogue (fused): +bias, 2x2 mean-pool, +residual, +bilinear upsample of a half-res
-// tensor, ELU, a second output (value + res2), and per-tile InstanceNorm++ statistics.
+// tensor, ELU, a second output (value + res2), and per-128-pixel InstanceNorm++ statistics
+// (mean, M2) of every output channel.
 #include <type_traits>
 
 #include "common.h"
@@ -29,30 +39,38 @@ namespace sdp {
 
 constexpr int PSTRIDE = 144;  // bytes per staged patch pixel: 32 ch x (hi,lo bf16) or 32 x f32, + 16 pad
 
-template <int TC, int KS>
+template <int WM, int TC, int KS>
 struct ConvTile {
-  static constexpr int TR = 128 / TC;
+  static constexpr int WN = 4 / WM;                // waves along N
+  static constexpr int RW = 128 / TC;              // pixel rows per wave
+  static constexpr int TR = WM * RW;               // tile rows
+  static constexpr int NTILE = WN * 64;            // output channels per workgroup
   static constexpr int HALO = KS == 3 ? 1 : 0;
   static constexpr int PC = TC + 2 * HALO;
   static constexpr int PR = TR + 2 * HALO;
   static constexpr int NPIX = PR * PC;
   static constexpr int NU = (NPIX * 8 + 255) / 256;            // 16-B staging units per thread per chunk
-  static constexpr int PATCH_BYTES = NPIX * PSTRIDE;            // transformed (hi|lo or f32) patch
+  static constexpr int PATCH_BYTES = NU * 32 * PSTRIDE;         // one transformed patch (+ slack: every
+                                                                //   staging unit has a pixel slot)
   static constexpr int RAW_BYTES = NU * 256 * 16;               // raw fp32 patch landed by LDS-DMA
-  static constexpr int LDS_BYTES = PATCH_BYTES + RAW_BYTES;
+  static constexpr int LDS_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
 SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-template <int MODE, int TC, int KS, bool POOL>
-__global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
+template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
+__global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
-  using T = ConvTile<TC, KS>;
+  using T = ConvTile<WM, TC, KS>;
   constexpr int NT = KS * KS;
+  constexpr int NU = T::NU;
+  constexpr int XT = NT >= 4 ? 4 : NT;            // taps that carry the transform of the next chunk
   __shared__ __attribute__((aligned(16))) char lds[T::LDS_BYTES];
+  char* const raw = lds + 2 * T::PATCH_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = WM == 1 ? 0 : (wave & 1), wn = WM == 1 ? wave : (wave >> 1);
   const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
   const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c;
   int t = blockIdx.x;
@@ -63,22 +81,21 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   t -= ph * tiles_rc;
   const int ph_r = ph / d, ph_c = ph - (ph / d) * d;
   const int sr0 = (t / tiles_c) * T::TR, sc0 = (t % tiles_c) * TC;
-  const int n0 = blockIdx.y * 128;
-  const int trow0 = (TC == 64) ? 0 : 2 * wm;      // wave's 2 output rows: trow0, trow0+1
-  const int tcol0 = (TC == 64) ? 32 * wm : 0;     // wave's 32 output columns
+  const int n0 = blockIdx.y * T::NTILE;
+  const int wrow0 = wm * T::RW;                    // wave's first tile row
 
   const int Cin = a.Cin, Cout = a.Cout;
   const int nchunks = Cin / 32;
   const int NB = Cout / 32;
   const int nbg0 = n0 / 32 + wn * 2;               // global 32-channel block of this wave's nb=0
 
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
+  f32x16 acc[4][2];
+  static_for<0, 4>([&](auto i) {
+    static_for<0, 2>([&](auto j) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    });
+  });
 
   // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
   // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
@@ -96,24 +113,31 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
     });
   };
-  load_b(std::integral_constant<int, 0>{}, 0, 0);
 
   const float* inb = a.in + (size_t)b * a.H * a.W * Cin;
-  // scale/shift rows of this image; when there is no affine prologue point at any valid
-  // memory (loads below are unconditional, their values unused)
-  const float* ssb = a.pro_ss ? a.pro_ss + (size_t)b * Cin * 2 : a.in;
+  // (scale, shift) rows of this image; without an affine prologue the (unconditional) loads
+  // read valid memory and the values are replaced by the identity (1, 0)
+  const bool affine = a.pro_ss != nullptr;
+  const float* ssb = affine ? a.pro_ss + (size_t)b * Cin * 2 : a.in;
+  const int my_cv = tid & 7;                        // every unit of a thread has cv == tid % 8
+  const int a_lane_off = (lane & 31) * PSTRIDE + (lane >> 5) * 16;
+  float4 ssv0, ssv1;                                // (scale, shift) of this thread's 4 channels
+  auto load_ss = [&](int chunk) __attribute__((always_inline)) {
+    const float4 s0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
+    const float4 s1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
+    ssv0 = affine ? s0 : make_float4(1.f, 0.f, 1.f, 0.f);
+    ssv1 = affine ? s1 : make_float4(1.f, 0.f, 1.f, 0.f);
+  };
 
-  // ---- patch staging, software-pipelined: the next chunk's global loads are issued into
-  //      registers before this chunk's MFMA loop and written (prologue applied) after it ----
-  constexpr int NU = T::NU;
-  char* raw = lds + T::PATCH_BYTES;
-  float4 ssv0 = make_float4(1.f, 0.f, 1.f, 0.f), ssv1 = ssv0;   // (scale, shift) of this thread's 4 channels
-  const int my_cv = tid & 7;                                     // every unit of a thread has cv == tid % 8
   // Staging unit u = 16 B (4 channels) of one patch pixel.  Its byte offset inside the image
   // (clamped into range, so every load is unconditional) and its validity (zero padding)
   // depend only on the tile, so they are computed once; per chunk only the scalar channel
-  // offset changes.
-  const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, 0x7fffffff, 0x00020000);
+  // offset changes.  Unit u is landed by lane u%64 of wave (u%256)/64 -- the same thread
+  // that transforms it, so raw needs no barrier, only the DMA's vmcnt.
+  // num_records = the image's bytes: the (unconditional) DMA of a chunk past the last one
+  // reads zeros instead of running off the tensor
+  const __amdgpu_buffer_rsrc_t irs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, a.H * a.W * Cin * 4, 0x00020000);
   int uoff[NU];
   unsigned uvalid = 0;
   static_for<0, NU>([&](auto kc) {
@@ -136,135 +160,216 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
     uoff[k] = ((y * a.W + x) * Cin + cv * 4) * 4;   // bytes, < 2^31 for every admitted shape
     uvalid |= (valid ? 1u : 0u) << k;
   });
-  // LDS-DMA of staging unit k (no VGPR destination): lane i of a wave lands 16 B at the
-  // wave-uniform base + 16*i, i.e. unit u at raw + 16*u
+  // LDS-DMA of staging unit k: lane i of a wave lands 16 B at the wave-uniform base + 16*i
   auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
-    if ((tid & ~63) + k * 256 >= T::NPIX * 8) return;   // whole wave past the patch (wave-uniform)
     const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
         uoff[k], chunk * 128, 0, 0);
   };
-  auto load_ss = [&](int chunk) __attribute__((always_inline)) {
-    ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
-    ssv1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
+  // transform staging unit k of raw into patch buffer PB
+  // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
+  auto xform_load = [&](auto kc) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    return *reinterpret_cast<const float4*>(raw + (tid + k * 256) * 16);
   };
-  auto write_patch = [&]() __attribute__((always_inline)) {
-    static_for<0, NU>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      const int u = tid + k * 256;
-      if (u >= T::NPIX * 8) return;
-      const int pix = u >> 3, cv = u & 7;
-      float4 v = *reinterpret_cast<const float4*>(raw + u * 16);
-      const bool valid = (uvalid >> k) & 1u;
-      if (!valid) v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (valid) {
-        if (a.pro_mode == PRO_AFFINE_ELU) {
-          v.x = elu(fmaf(v.x, ssv0.x, ssv0.y));
-          v.y = elu(fmaf(v.y, ssv0.z, ssv0.w));
-          v.z = elu(fmaf(v.z, ssv1.x, ssv1.y));
-          v.w = elu(fmaf(v.w, ssv1.z, ssv1.w));
-        } else if (a.pro_mode == PRO_ELU) {
-          v.x = elu(v.x); v.y = elu(v.y); v.z = elu(v.z); v.w = elu(v.w);
-        }
+  auto xform_store = [&](auto kc, auto pb, float4 v) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int PB = decltype(pb)::value;
+    const int pix = (tid + k * 256) >> 3;   // units past the patch land in its slack: no branch
+    v.x = fmaf(v.x, ssv0.x, ssv0.y);
+    v.y = fmaf(v.y, ssv0.z, ssv0.w);
+    v.z = fmaf(v.z, ssv1.x, ssv1.y);
+    v.w = fmaf(v.w, ssv1.z, ssv1.w);
+    if constexpr (PELU) {
+      v.x = elu_max(v.x); v.y = elu_max(v.y); v.z = elu_max(v.z); v.w = elu_max(v.w);
+    }
+    if constexpr (POOL) {   // ConvMeanPool is the only zero-padded conv (layers.py:291-313)
+      if (!((uvalid >> k) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE;
+    if constexpr (MODE == MODE_F32) {
+      *reinterpret_cast<float4*>(dst + my_cv * 16) = v;
+    } else {
+      bf16x4 hi;
+      hi[0] = (__bf16)v.x; hi[1] = (__bf16)v.y; hi[2] = (__bf16)v.z; hi[3] = (__bf16)v.w;
+      *reinterpret_cast<bf16x4*>(dst + my_cv * 8) = hi;
+      if constexpr (MODE == MODE_F32X3) {
+        bf16x4 lo;
+        lo[0] = (__bf16)(v.x - (float)hi[0]);
+        lo[1] = (__bf16)(v.y - (float)hi[1]);
+        lo[2] = (__bf16)(v.z - (float)hi[2]);
+        lo[3] = (__bf16)(v.w - (float)hi[3]);
+        *reinterpret_cast<bf16x4*>(dst + 64 + my_cv * 8) = lo;
       }
-      char* dst = lds + pix * PSTRIDE;
-      if constexpr (MODE == MODE_F32) {
-        *reinterpret_cast<float4*>(dst + cv * 16) = v;
-      } else {
-        bf16x4 hi, lo;
-        hi[0] = (__bf16)v.x; hi[1] = (__bf16)v.y; hi[2] = (__bf16)v.z; hi[3] = (__bf16)v.w;
-        *reinterpret_cast<bf16x4*>(dst + cv * 8) = hi;
-        if constexpr (MODE == MODE_F32X3) {
-          lo[0] = (__bf16)(v.x - (float)hi[0]);
-          lo[1] = (__bf16)(v.y - (float)hi[1]);
-          lo[2] = (__bf16)(v.z - (float)hi[2]);
-          lo[3] = (__bf16)(v.w - (float)hi[3]);
-          *reinterpret_cast<bf16x4*>(dst + 64 + cv * 8) = lo;
-        }
-      }
+    }
+  };
+  auto xform_unit = [&](auto kc, auto pb) __attribute__((always_inline)) { xform_store(kc, pb, xform_load(kc)); };
+  // half of unit k (channels 2h, 2h+1 of its 4): prologue + bf16 hi/lo split + one ds_write2
+  auto xform_piece = [&](auto kc, auto hc, auto pb, float4 v4) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value, h = decltype(hc)::value, PB = decltype(pb)::value;
+    const int pix = (tid + k * 256) >> 3;
+    float x0 = h ? v4.z : v4.x, x1 = h ? v4.w : v4.y;
+    const float4 sv = h ? ssv1 : ssv0;
+    x0 = fmaf(x0, sv.x, sv.y);
+    x1 = fmaf(x1, sv.z, sv.w);
+    if constexpr (PELU) {
+      x0 = elu_max(x0);
+      x1 = elu_max(x1);
+    }
+    if constexpr (POOL) {
+      const bool ok = (uvalid >> k) & 1u;
+      x0 = ok ? x0 : 0.f;
+      x1 = ok ? x1 : 0.f;
+    }
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    bf16x2 hi;
+    hi[0] = (__bf16)x0;
+    hi[1] = (__bf16)x1;
+    char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 8 + h * 4;
+    *reinterpret_cast<bf16x2*>(dst) = hi;
+    if constexpr (MODE == MODE_F32X3) {
+      bf16x2 lo;
+      lo[0] = (__bf16)(x0 - (float)hi[0]);
+      lo[1] = (__bf16)(x1 - (float)hi[1]);
+      *reinterpret_cast<bf16x2*>(dst + 64) = lo;
+    }
+  };
+
+  // ---- prologue: chunk 0 staged + transformed, chunk 1 in flight ----
+  load_b(std::integral_constant<int, 0>{}, 0, 0);
+  load_ss(0);
+  static_for<0, NU>([&](auto k) { load_unit(k, 0); });
+  static_for<0, NU>([&](auto k) { xform_unit(k, std::integral_constant<int, 0>{}); });
+  if (nchunks > 1) {
+    load_ss(1);
+    static_for<0, NU>([&](auto k) { load_unit(k, 1); });
+  }
+  __syncthreads();
+
+  // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel
+  auto read_a = [&](const char* pat, auto tap_c, auto s_c, bf16x8* hi, bf16x8* lo) __attribute__((always_inline)) {
+    constexpr int tap = decltype(tap_c)::value, s = decltype(s_c)::value;
+    constexpr int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
+    static_for<0, 4>([&](auto mbc) {
+      constexpr int mb = decltype(mbc)::value;
+      constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
+      const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off + s * 32;
+      hi[mb] = *reinterpret_cast<const bf16x8*>(src);
+      if constexpr (MODE == MODE_F32X3) lo[mb] = *reinterpret_cast<const bf16x8*>(src + 64);
     });
   };
 
-  load_ss(0);
-  static_for<0, NU>([&](auto k) { load_unit(k, 0); });
   auto do_chunk = [&](auto parity, int chunk) __attribute__((always_inline)) {
     constexpr int P = decltype(parity)::value;
-    __syncthreads();
-    write_patch();
-    __syncthreads();
-    const bool more = chunk + 1 < nchunks;
-
-    // ---- 9 (or 1) taps over the staged patch; per tap: prefetch the next tap's weight
-    //      fragments, issue a slice of the next chunk's patch loads, then the MFMAs ----
+    // The transform of chunk+1 and the DMA of chunk+2 run unconditionally (branch-free
+    // regions schedule across the MFMAs); past the last chunk they touch only dead buffers.
+    const char* pat = lds + P * T::PATCH_BYTES;
+    bf16x8 pre_hi[4], pre_lo[4];   // s=0 fragments of the next tap, read one region ahead
+    if constexpr (MODE != MODE_F32) read_a(pat, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                                           pre_hi, pre_lo);
     static_for<0, NT>([&](auto tap_c) {
       constexpr int tap = decltype(tap_c)::value;
       constexpr int CUR = (tap + P) & 1, NXT = (tap + 1 + P) & 1;
       if constexpr (tap + 1 < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + 1);
-      else if (more) load_b(std::integral_constant<int, NXT>{}, chunk + 1, 0);
-      if (more) {
-        if constexpr (tap == 0) load_ss(chunk + 1);
-        static_for<0, NU>([&](auto kc) {
-          if constexpr (decltype(kc)::value % NT == tap) load_unit(kc, chunk + 1);
-        });
-      }
-      // keep the prefetches ahead of this tap's MFMAs (hipcc otherwise sinks them to the end
-      // of the tap, exposing their latency at the next tap)
+      else load_b(std::integral_constant<int, NXT>{}, min(chunk + 1, nchunks - 1), 0);
       __builtin_amdgcn_sched_barrier(0);
-      const int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
+      // next chunk's transform on taps [0, XT), then the chunk after next's DMA on the rest
+      // this tap's share of the next chunk's transform (units k with k % XT == tap)
+      constexpr int NX = (tap < XT) ? (NU - tap + XT - 1) / XT : 0;
+      float4 xv[NX > 0 ? NX : 1];
+      auto xform_loads = [&]() __attribute__((always_inline)) {
+        static_for<0, NX>([&](auto j) { xv[j] = xform_load(std::integral_constant<int, tap + XT * j>{}); });
+      };
+      auto xform_stores = [&]() __attribute__((always_inline)) {
+        static_for<0, NX>([&](auto j) {
+          xform_store(std::integral_constant<int, tap + XT * j>{}, std::integral_constant<int, 1 - P>{}, xv[j]);
+        });
+      };
+      auto dmas = [&]() __attribute__((always_inline)) {
+        if constexpr (tap == NT - 1) load_ss(min(chunk + 2, nchunks - 1));
+        static_for<0, NU>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          constexpr int dt = NT > XT ? XT + k % (NT - XT) : 0;
+          if constexpr (dt == tap) load_unit(kc, chunk + 2);
+        });
+      };
       if constexpr (MODE == MODE_F32) {
-        float av[2][16];
+        xform_loads();
+        xform_stores();
+        if constexpr (NT == 1) __builtin_amdgcn_sched_barrier(0);
+        dmas();
+        const int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
 #pragma unroll
-        for (int mb = 0; mb < 2; ++mb) {
-          const int pix = (trow0 + mb + kh) * T::PC + tcol0 + (lane & 31) + kw;
-          const char* src = lds + pix * PSTRIDE + (lane >> 5) * 64;
+        for (int half = 0; half < 2; ++half) {   // k steps [8*half, 8*half+8)
+          float av[4][8];
+          static_for<0, 4>([&](auto mbc) {
+            constexpr int mb = decltype(mbc)::value;
+            constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
+            const int pix = (wrow0 + mr + kh) * T::PC + mc + (lane & 31) + kw;
+            const char* src = pat + pix * PSTRIDE + (lane >> 5) * 64 + half * 32;
+            const float4 f0 = *reinterpret_cast<const float4*>(src);
+            const float4 f1 = *reinterpret_cast<const float4*>(src + 16);
+            av[mb][0] = f0.x; av[mb][1] = f0.y; av[mb][2] = f0.z; av[mb][3] = f0.w;
+            av[mb][4] = f1.x; av[mb][5] = f1.y; av[mb][6] = f1.z; av[mb][7] = f1.w;
+          });
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float4 f = *reinterpret_cast<const float4*>(src + q * 16);
-            av[mb][4 * q + 0] = f.x; av[mb][4 * q + 1] = f.y; av[mb][4 * q + 2] = f.z; av[mb][4 * q + 3] = f.w;
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb) {
-            const uint4 bv = bq[CUR][nb][k >> 2];
-            const uint32_t bw = (k & 3) == 0 ? bv.x : (k & 3) == 1 ? bv.y : (k & 3) == 2 ? bv.z : bv.w;
-            const float bf = __uint_as_float(bw);
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb)
-              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mb][k], bf, acc[mb][nb], 0, 0, 0);
+          for (int kk = 0; kk < 8; ++kk) {
+            const int k = half * 8 + kk;
+            static_for<0, 2>([&](auto nbc) {
+              constexpr int nb = decltype(nbc)::value;
+              const uint4 bv = bq[CUR][nb][k >> 2];
+              const uint32_t bw = (k & 3) == 0 ? bv.x : (k & 3) == 1 ? bv.y : (k & 3) == 2 ? bv.z : bv.w;
+              const float bf = __uint_as_float(bw);
+              static_for<0, 4>([&](auto mbc) {
+                constexpr int mb = decltype(mbc)::value;
+                acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mb][kk], bf, acc[mb][nb], 0, 0, 0);
+              });
+            });
           }
         }
       } else {
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          bf16x8 ahi[2], alo[2];
-#pragma unroll
-          for (int mb = 0; mb < 2; ++mb) {
-            const int pix = (trow0 + mb + kh) * T::PC + tcol0 + (lane & 31) + kw;
-            const char* src = lds + pix * PSTRIDE + s * 32 + (lane >> 5) * 16;
-            ahi[mb] = *reinterpret_cast<const bf16x8*>(src);
-            if constexpr (MODE == MODE_F32X3) alo[mb] = *reinterpret_cast<const bf16x8*>(src + 64);
+        // Explicitly interleaved: 16 blocks of (s, nb, mb) -> 3 MFMAs (fp32x3) each, every
+        // block its own scheduling region carrying one piece (2 channels) of the next chunk's
+        // transform, so the VALU issues in the MFMA shadow.  Reads: this tap's raw units
+        // first (their lgkmcnt retires first), then A(tap, s=1), then A(tap+1, s=0).
+        float4 xv[NX > 0 ? NX : 1];
+        static_for<0, NX>([&](auto j) { xv[j] = xform_load(std::integral_constant<int, tap + XT * j>{}); });
+        bf16x8 c0_hi[4], c0_lo[4], c1_hi[4], c1_lo[4];
+        static_for<0, 4>([&](auto mb) {
+          c0_hi[mb] = pre_hi[mb];
+          if constexpr (MODE == MODE_F32X3) c0_lo[mb] = pre_lo[mb];
+        });
+        read_a(pat, tap_c, std::integral_constant<int, 1>{}, c1_hi, c1_lo);
+        if constexpr (tap + 1 < NT)
+          read_a(pat, std::integral_constant<int, tap + 1>{}, std::integral_constant<int, 0>{}, pre_hi, pre_lo);
+        if constexpr (NT > 1) dmas();   // 1x1: after the blocks, behind this tap's raw reads
+        static_for<0, 16>([&](auto blk_c) {
+          constexpr int blk = decltype(blk_c)::value;
+          constexpr int s = blk >> 3, nb = (blk >> 2) & 1, mb = blk & 3;
+          const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
+          const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
+          const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
+          const bf16x8 ahi = s == 0 ? c0_hi[mb] : c1_hi[mb];
+          if constexpr (MODE == MODE_F32X3) {
+            const bf16x8 alo = s == 0 ? c0_lo[mb] : c1_lo[mb];
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[mb][nb], 0, 0, 0);
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[mb][nb], 0, 0, 0);
           }
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb) {
-            const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
-            const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
-            const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
-#pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
-              if constexpr (MODE == MODE_F32X3) {
-                acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[mb], bhi, acc[mb][nb], 0, 0, 0);
-                acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], blo, acc[mb][nb], 0, 0, 0);
-              }
-              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[mb], bhi, acc[mb][nb], 0, 0, 0);
-            }
-          }
-        }
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[mb][nb], 0, 0, 0);
+          if constexpr (blk < 2 * NX) xform_piece(std::integral_constant<int, tap + XT * (blk >> 1)>{},
+                                                  std::integral_constant<int, blk & 1>{},
+                                                  std::integral_constant<int, 1 - P>{}, xv[blk >> 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        if constexpr (NT == 1) dmas();
       }
     });
+    // patch[P] free for chunk+2's transform, patch[1-P] complete.  A raw barrier: only the
+    // LDS writes must have landed; the DMA of chunk+2 and the weight loads stay in flight.
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
   };
   static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
   for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
@@ -276,32 +381,15 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
   // C/D layout of 32x32 MFMA: col (N) = lane&31, row (M) = (r&3) + 8*(r>>2) + 4*(lane>>5)
   const int col_lane = lane & 31;
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
-  constexpr int NV = POOL ? 8 : 32;  // values per lane per nb
-  // per-lane Welford state over this lane's NV outputs of each channel (InstanceNorm++ stats)
+  // per-lane Welford state over this lane's outputs of each channel (InstanceNorm++ stats)
   float wmean[2] = {0.f, 0.f}, wm2[2] = {0.f, 0.f};
-#pragma unroll
-  for (int nb = 0; nb < 2; ++nb) {
+  int cnt = 0;
+  static_for<0, 2>([&](auto nbc) {
+    constexpr int nb = decltype(nbc)::value;
     const int co = n0 + wn * 64 + nb * 32 + col_lane;
     const float bias = a.bias ? a.bias[co] : 0.f;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      float v;
-      int y, x;
-      if constexpr (POOL) {
-        const int r = 2 * i;  // regs r, r+1 hold adjacent columns
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const float o00 = acc[0][nb][r] + bias, o10 = acc[1][nb][r] + bias;
-        const float o01 = acc[0][nb][r + 1] + bias, o11 = acc[1][nb][r + 1] + bias;
-        v = (((o00 + o10) + o01) + o11) / 4.0f;  // layers.py:310-312 summation order
-        y = (sr0 + trow0) >> 1;
-        x = (sc0 + tcol0 + m) >> 1;
-      } else {
-        const int mb = i >> 4, r = i & 15;
-        const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        v = acc[mb][nb][r] + bias;
-        y = (sr0 + trow0 + mb) * d + ph_r;
-        x = (sc0 + tcol0 + m) * d + ph_c;
-      }
+    cnt = 0;
+    auto emit = [&](float v, int y, int x) __attribute__((always_inline)) {
       const size_t oidx = (((size_t)b * Ho + y) * Wo + x) * Cout + co;
       if (a.up) {
         // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor at (y, x)
@@ -320,62 +408,86 @@ __global__ __launch_bounds__(256, 2) void conv_mfma_kernel(ConvArgs a) {
       if (a.out2) a.out2[oidx] = v + a.res2[oidx];
       if (a.epi_elu) v = elu(v);
       a.out[oidx] = v;
+      ++cnt;
       const float delta = v - wmean[nb];
-      wmean[nb] = fmaf(delta, 1.0f / (float)(i + 1), wmean[nb]);
+      wmean[nb] = fmaf(delta, 1.0f / (float)cnt, wmean[nb]);
       wm2[nb] = fmaf(delta, v - wmean[nb], wm2[nb]);
-      // keep the compiler from hoisting every epilogue load at once (VGPR spills)
-      if ((i & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    };
+    if constexpr (POOL) {
+      static_assert(TC == 64 && WM == 1, "pooling tiles: 2 rows x 64 columns per wave");
+      // frags mb (row 0) and mb+2 (row 1) hold vertically adjacent pixels; regs r, r+1 hold
+      // horizontally adjacent ones
+      static_for<0, 2>([&](auto mbc) {
+        constexpr int mb = decltype(mbc)::value;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = 2 * i;
+          const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          const float o00 = acc[mb][nb][r] + bias, o10 = acc[mb + 2][nb][r] + bias;
+          const float o01 = acc[mb][nb][r + 1] + bias, o11 = acc[mb + 2][nb][r + 1] + bias;
+          const float v = (((o00 + o10) + o01) + o11) / 4.0f;  // layers.py:310-312 summation order
+          emit(v, (sr0 + wrow0) >> 1, (sc0 + mb * 32 + m) >> 1);
+          if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+    } else {
+      static_for<0, 4>([&](auto mbc) {
+        constexpr int mb = decltype(mbc)::value;
+        constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          emit(acc[mb][nb][r] + bias, (sr0 + wrow0 + mr) * d + ph_r, (sc0 + mc + m) * d + ph_c);
+          // keep the compiler from hoisting every epilogue load at once
+          if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        }
+      });
     }
-  }
+  });
 
   if (a.stats) {
-    // Chan merge of equal-count partials: lanes l/l+32 (NV each), then waves wm=0/1 via LDS.
-    constexpr float CNT = POOL ? 32.f : 128.f;
-    float* red = reinterpret_cast<float*>(lds);  // [wn][nb][wm][32][2]
-    __syncthreads();
-#pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
+    // per wave = one 128-pixel group: Chan merge of lanes l / l+32 (equal counts)
+    const int group = tile * WM + wm;
+    const float n = (float)cnt;
+    static_for<0, 2>([&](auto nbc) {
+      constexpr int nb = decltype(nbc)::value;
       const float om = __shfl_xor(wmean[nb], 32), o2 = __shfl_xor(wm2[nb], 32);
       const float dm = om - wmean[nb];
       const float mean = 0.5f * (wmean[nb] + om);
-      const float m2 = wm2[nb] + o2 + dm * dm * (0.5f * NV);
+      const float m2 = wm2[nb] + o2 + dm * dm * (0.5f * n);
       if (lane < 32) {
-        float* r = red + (((wn * 2 + nb) * 2 + wm) * 32 + lane) * 2;
-        r[0] = mean;
-        r[1] = m2;
-      }
-    }
-    __syncthreads();
-    if (wm == 0 && lane < 32) {
-#pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const float* r0 = red + (((wn * 2 + nb) * 2 + 0) * 32 + lane) * 2;
-        const float* r1 = red + (((wn * 2 + nb) * 2 + 1) * 32 + lane) * 2;
-        const float dm = r1[0] - r0[0];
-        const float mean = 0.5f * (r0[0] + r1[0]);
-        const float m2 = r0[1] + r1[1] + dm * dm * (0.25f * CNT);
         const int co = n0 + wn * 64 + nb * 32 + lane;
-        float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.tiles_per_img + tile) * Cout + co;
+        float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + group) * Cout + co;
         *st = make_float2(mean, m2);
       }
-    }
+    });
   }
 #endif
 }
 
 // ----------------------------------------------------------------------------- launch
-template <int MODE, int TC, int KS, bool POOL>
-static hipError_t launch_t(const ConvArgs& a, hipStream_t st) {
-  dim3 grid(a.B * a.tiles_per_img, a.Cout / 128);
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, TC, KS, POOL>), grid, dim3(256), 0, st, a);
+template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
+static hipError_t launch_t(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<WM, TC, KS>;
+  a.tiles_per_img = a.H * a.W / (T::TR * TC);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, PELU>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
+template <int MODE, bool PELU>
+static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
+  if (ks == 1) return launch_t<MODE, 1, 64, 1, true, PELU>(a, st);   // only the ConvMeanPool 1x1 shortcut
+  if (pool) return launch_t<MODE, 1, 64, 3, true, PELU>(a, st);
+  if (wm == 2) return launch_t<MODE, 2, 32, 3, false, PELU>(a, st);
+  return tc == 64 ? launch_t<MODE, 1, 64, 3, false, PELU>(a, st) : launch_t<MODE, 1, 32, 3, false, PELU>(a, st);
+}
+
 template <int MODE>
-static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int tc, hipStream_t st) {
-  if (ks == 1) return launch_t<MODE, 64, 1, true>(a, st);   // only the ConvMeanPool 1x1 shortcut
-  if (pool) return tc == 64 ? launch_t<MODE, 64, 3, true>(a, st) : launch_t<MODE, 32, 3, true>(a, st);
-  return tc == 64 ? launch_t<MODE, 64, 3, false>(a, st) : launch_t<MODE, 32, 3, false>(a, st);
+static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
+  return a.pro_mode == PRO_NONE ? launch_elu<MODE, false>(a, ks, pool, wm, tc, st)
+                                : launch_elu<MODE, true>(a, ks, pool, wm, tc, st);
 }
 
 // Host entry: validates the shape contract the kernel's indexing assumes, then launches.
@@ -384,19 +496,25 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (a.Cin % 64 || a.Cout % 128) { *why = "conv: Cin%64 and Cout%128 required"; return hipErrorInvalidValue; }
   if (a.H % d || a.W % d) { *why = "conv: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
   const int Hs = a.H / d, Ws = a.W / d;
-  int tc = (Ws % 64 == 0) ? 64 : 32;
-  if (ks == 1) tc = 64;
-  const int tr = 128 / tc;
-  if (Ws % tc || Hs % tr) { *why = "conv: sub-grid not divisible by the 128-pixel tile"; return hipErrorInvalidValue; }
+  // 256-channel outputs: 128 px x 256 Cout tiles; 128-channel outputs: 256 px x 128 Cout
+  const int wm = (a.Cout % 256 == 0) ? 1 : 2;
+  int tc = (wm == 2) ? 32 : ((Ws % 64 == 0) ? 64 : 32);
+  if (ks == 1 || pool) tc = 64;
+  const int tr = wm * 128 / tc;
+  if (Ws % tc || Hs % tr) { *why = "conv: sub-grid not divisible by the pixel tile"; return hipErrorInvalidValue; }
   if (ks == 1 && !pool) { *why = "conv: 1x1 only as the pooled shortcut"; return hipErrorInvalidValue; }
-  if (pool && (d != 1 || (a.H & 1) || (a.W & 1))) { *why = "conv: pooling needs d=1, even H,W"; return hipErrorInvalidValue; }
+  if (pool && (d != 1 || wm != 1 || (a.H & 1) || (a.W & 1))) {
+    *why = "conv: pooling needs d=1, even H,W and 256-multiple Cout";
+    return hipErrorInvalidValue;
+  }
   if (a.up && ((a.H & 1) || (a.W & 1) || a.H < 2 || a.W < 2)) { *why = "conv: upsample needs even H,W"; return hipErrorInvalidValue; }
   if (!a.circular && d != 1) { *why = "conv: zero padding only for d=1"; return hipErrorInvalidValue; }
-  a.tiles_per_img = a.H * a.W / 128;
+  if (a.pro_mode == PRO_AFFINE_ELU && !a.pro_ss) { *why = "conv: affine prologue without scale/shift"; return hipErrorInvalidValue; }
+  if (a.pro_mode != PRO_AFFINE_ELU) a.pro_ss = nullptr;
   switch (mode) {
-    case MODE_F32: return launch_mode<MODE_F32>(a, ks, pool, tc, st);
-    case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, tc, st);
-    default: return launch_mode<MODE_BF16>(a, ks, pool, tc, st);
+    case MODE_F32: return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
+    case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
+    default: return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st);
   }
 }
 
