@@ -42,12 +42,15 @@ struct ConvArgs {
   float* out2;             // optional second output: value + res2 (CRP running sum)
   const float* res2;
   const float* up;         // [B][H/2][W/2][Cout]: bilinear(align_corners) upsample-add, or null
-  const float* pro_ss;     // [B][Cin][2] (scale, shift) for PRO_AFFINE_ELU
+  const float* pro_ss;     // [B][Cin][2] (scale, shift) of the prologue: InstanceNorm++ affine, or the
+                           // identity (1, 0) table with ss_bstride = 0
+  int ss_bstride;          // floats between the rows of consecutive images
   float* stats;            // [B][groups_per_img][Cout][2] per-128-pixel (mean, M2) or null
   int B, H, W, Cin, Cout;
   int dil, circular, pro_mode, epi_elu;
   int tiles_per_img;       // workgroup tiles per image (set by the launcher)
   int groups_per_img;      // 128-pixel statistics groups per image (H*W/128)
+  unsigned long long* dbg; // diagnostics builds only (SDP_TIMING): per-workgroup phase clocks
 };
 
 }  // namespace sdp

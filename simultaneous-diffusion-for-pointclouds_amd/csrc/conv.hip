@@ -37,6 +37,18 @@
 
 namespace sdp {
 
+// Diagnostic knock-outs for tools/conv_bench (never set in the library build):
+// 1 = no patch DMA, 2 = no transform, 4 = no weight loads, 8 = no chunk barrier, 16 = no epilogue
+#ifndef SDP_KO
+#define SDP_KO 0
+#endif
+
+#ifdef SDP_TIMING   // tools/conv_bench: per-workgroup phase clocks of wave 0 into a.dbg
+#define SDP_T(i) do { if (tid == 0) tclk[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define SDP_T(i) do { } while (0)
+#endif
+
 constexpr int PSTRIDE = 144;  // bytes per staged patch pixel: 32 ch x (hi,lo bf16) or 32 x f32, + 16 pad
 
 template <int WM, int TC, int KS>
@@ -53,7 +65,9 @@ struct ConvTile {
   static constexpr int PATCH_BYTES = NU * 32 * PSTRIDE;         // one transformed patch (+ slack: every
                                                                 //   staging unit has a pixel slot)
   static constexpr int RAW_BYTES = NU * 256 * 16;               // raw fp32 patch landed by LDS-DMA
-  static constexpr int LDS_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
+  static constexpr int PIPE_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
+  static constexpr int EPI_BYTES = WM * 64 * (NTILE + 8) * 4;   // epilogue staging (one half)
+  static constexpr int LDS_BYTES = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -70,10 +84,18 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   char* const raw = lds + 2 * T::PATCH_BYTES;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef SDP_TIMING
+  unsigned long long tclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tbar = 0;
+#endif
+  SDP_T(0);
   const int wm = WM == 1 ? 0 : (wave & 1), wn = WM == 1 ? wave : (wave >> 1);
   const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
   const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c;
-  int t = blockIdx.x;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so give each XCD a
+  // contiguous range of tiles -- vertically adjacent tiles share their halo rows in its L2
+  const int nwg = gridDim.x;
+  int t = (nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3);
   const int b = t / a.tiles_per_img;
   const int tile = t - b * a.tiles_per_img;
   t = tile;
@@ -102,9 +124,13 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wf, 0, 0x7fffffff, 0x00020000);
   const int wv0 = ((nbg0 + 0) * 64 + lane) * 64, wv1 = ((nbg0 + 1) * 64 + lane) * 64;
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-  uint4 bq[2][2][4];
+  // weight fragment ring: 3 taps deep (prefetch distance 2) when the tap count is a multiple
+  // of 3, so the slot of (chunk, tap) is tap % 3 in every chunk; 2 deep for the 1x1 conv
+  constexpr int NBUF = (NT % 3 == 0) ? 3 : 2;
+  uint4 bq[NBUF][2][4];
   auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
     constexpr int J = decltype(buf)::value;
+    if constexpr (SDP_KO & 4) return;
     const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096);
     static_for<0, 4>([&](auto q) {
       const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
@@ -115,18 +141,15 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   };
 
   const float* inb = a.in + (size_t)b * a.H * a.W * Cin;
-  // (scale, shift) rows of this image; without an affine prologue the (unconditional) loads
-  // read valid memory and the values are replaced by the identity (1, 0)
-  const bool affine = a.pro_ss != nullptr;
-  const float* ssb = affine ? a.pro_ss + (size_t)b * Cin * 2 : a.in;
+  // (scale, shift) rows of this image (the identity table when there is no affine prologue):
+  // consumed only by the next chunk's transform, so the loads stay in flight across a chunk
+  const float* ssb = a.pro_ss + (size_t)b * a.ss_bstride;
   const int my_cv = tid & 7;                        // every unit of a thread has cv == tid % 8
   const int a_lane_off = (lane & 31) * PSTRIDE + (lane >> 5) * 16;
   float4 ssv0, ssv1;                                // (scale, shift) of this thread's 4 channels
   auto load_ss = [&](int chunk) __attribute__((always_inline)) {
-    const float4 s0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
-    const float4 s1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
-    ssv0 = affine ? s0 : make_float4(1.f, 0.f, 1.f, 0.f);
-    ssv1 = affine ? s1 : make_float4(1.f, 0.f, 1.f, 0.f);
+    ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
+    ssv1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
   };
 
   // Staging unit u = 16 B (4 channels) of one patch pixel.  Its byte offset inside the image
@@ -163,6 +186,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   // LDS-DMA of staging unit k: lane i of a wave lands 16 B at the wave-uniform base + 16*i
   auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
+    if constexpr (SDP_KO & 1) return;
     const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
@@ -209,6 +233,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   // half of unit k (channels 2h, 2h+1 of its 4): prologue + bf16 hi/lo split + one ds_write2
   auto xform_piece = [&](auto kc, auto hc, auto pb, float4 v4) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value, h = decltype(hc)::value, PB = decltype(pb)::value;
+    if constexpr (SDP_KO & 2) return;
     const int pix = (tid + k * 256) >> 3;
     float x0 = h ? v4.z : v4.x, x1 = h ? v4.w : v4.y;
     const float4 sv = h ? ssv1 : ssv0;
@@ -237,8 +262,10 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     }
   };
 
+  SDP_T(1);
   // ---- prologue: chunk 0 staged + transformed, chunk 1 in flight ----
   load_b(std::integral_constant<int, 0>{}, 0, 0);
+  if constexpr (NBUF == 3) load_b(std::integral_constant<int, 1>{}, 0, 1);
   load_ss(0);
   static_for<0, NU>([&](auto k) { load_unit(k, 0); });
   static_for<0, NU>([&](auto k) { xform_unit(k, std::integral_constant<int, 0>{}); });
@@ -247,6 +274,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     static_for<0, NU>([&](auto k) { load_unit(k, 1); });
   }
   __syncthreads();
+  SDP_T(2);
 
   // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel
   auto read_a = [&](const char* pat, auto tap_c, auto s_c, bf16x8* hi, bf16x8* lo) __attribute__((always_inline)) {
@@ -271,9 +299,11 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
                                            pre_hi, pre_lo);
     static_for<0, NT>([&](auto tap_c) {
       constexpr int tap = decltype(tap_c)::value;
-      constexpr int CUR = (tap + P) & 1, NXT = (tap + 1 + P) & 1;
-      if constexpr (tap + 1 < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + 1);
-      else load_b(std::integral_constant<int, NXT>{}, min(chunk + 1, nchunks - 1), 0);
+      constexpr int DIST = NBUF - 1;                       // prefetch distance in taps
+      constexpr int CUR = NBUF == 3 ? tap % 3 : (tap + P) & 1;
+      constexpr int NXT = NBUF == 3 ? (tap + DIST) % 3 : (tap + 1 + P) & 1;
+      if constexpr (tap + DIST < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + DIST);
+      else load_b(std::integral_constant<int, NXT>{}, min(chunk + 1, nchunks - 1), tap + DIST - NT);
       __builtin_amdgcn_sched_barrier(0);
       // next chunk's transform on taps [0, XT), then the chunk after next's DMA on the rest
       // this tap's share of the next chunk's transform (units k with k % XT == tap)
@@ -291,7 +321,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         if constexpr (tap == NT - 1) load_ss(min(chunk + 2, nchunks - 1));
         static_for<0, NU>([&](auto kc) {
           constexpr int k = decltype(kc)::value;
-          constexpr int dt = NT > XT ? XT + k % (NT - XT) : 0;
+          constexpr int dt = NT > XT ? XT : 0;   // all at the first free tap: the longest flight
           if constexpr (dt == tap) load_unit(kc, chunk + 2);
         });
       };
@@ -368,8 +398,14 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     });
     // patch[P] free for chunk+2's transform, patch[1-P] complete.  A raw barrier: only the
     // LDS writes must have landed; the DMA of chunk+2 and the weight loads stay in flight.
+#ifdef SDP_TIMING
+    const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+#endif
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
+    if constexpr (!(SDP_KO & 8)) __builtin_amdgcn_s_barrier();
+#ifdef SDP_TIMING
+    tbar += __builtin_amdgcn_s_memtime() - tb0;
+#endif
   };
   static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
   for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
@@ -377,20 +413,78 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     do_chunk(std::integral_constant<int, 1>{}, chunk + 1);
   }
 
+  SDP_T(3);
   // ------------------------------------------------------------------ epilogue
-  // C/D layout of 32x32 MFMA: col (N) = lane&31, row (M) = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  const int col_lane = lane & 31;
+  // The accumulators go through LDS (the patch/raw buffers are free now) in two halves of
+  // 64 pixels per wave, so the output is written as whole pixel rows -- every thread owns 4
+  // consecutive channels of a pixel, every store/load is 16 B and a wave instruction covers
+  // 1 KiB (Cout 256) or two 512-B rows -- with bias, 2x2 mean-pool, residual, bilinear
+  // upsample-add, the CRP second output, ELU and the InstanceNorm++ statistics applied on
+  // the way.
+  __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
+  __syncthreads();
+  constexpr int SROW = T::NTILE + 8;               // staged row stride (floats): conflict-free writes
+  constexpr int SP = WM * 64;                      // staged pixels per half
+  constexpr int CG = T::NTILE / 4;                 // 16-B channel groups per pixel
+  constexpr int PL = 256 / CG;                     // threads per channel group
+  constexpr int NPO = POOL ? SP / 4 : SP;          // output pixels per half
+  static_assert(SP * SROW * 4 <= T::LDS_BYTES, "epilogue staging fits the LDS");
+  float* stage = reinterpret_cast<float*>(lds);
+  const int cg = tid % CG, pl = tid / CG;
+  const int co0 = n0 + cg * 4;                     // this thread's 4 output channels
+  const float4 bias4 = a.bias ? ld4(a.bias + co0) : make_float4(0.f, 0.f, 0.f, 0.f);
   const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
-  // per-lane Welford state over this lane's outputs of each channel (InstanceNorm++ stats)
-  float wmean[2] = {0.f, 0.f}, wm2[2] = {0.f, 0.f};
-  int cnt = 0;
-  static_for<0, 2>([&](auto nbc) {
-    constexpr int nb = decltype(nbc)::value;
-    const int co = n0 + wn * 64 + nb * 32 + col_lane;
-    const float bias = a.bias ? a.bias[co] : 0.f;
-    cnt = 0;
-    auto emit = [&](float v, int y, int x) __attribute__((always_inline)) {
-      const size_t oidx = (((size_t)b * Ho + y) * Wo + x) * Cout + co;
+  float* outb = a.out + (size_t)b * Ho * Wo * Cout;
+  // shifted sums per (stats group, channel): K = the thread's first value
+  float4 sK[WM], s1[WM], s2[WM];
+  int sn[WM];
+  static_for<0, WM>([&](auto g) {
+    sK[g] = make_float4(0.f, 0.f, 0.f, 0.f); s1[g] = sK[g]; s2[g] = sK[g]; sn[g] = 0;
+  });
+  static_for<0, 2>([&](auto hc) {
+    constexpr int h = decltype(hc)::value;
+    // ---- stage this half's accumulators: wave (wm, wn), fragments mb of the half
+    static_for<0, 2>([&](auto ic) {
+      constexpr int mb = POOL ? (h + 2 * decltype(ic)::value) : (2 * h + decltype(ic)::value);
+      constexpr int q0 = decltype(ic)::value * 32;
+      static_for<0, 2>([&](auto nbc) {
+        constexpr int nb = decltype(nbc)::value;
+        float* dst = stage + (wm * 64 + q0 + 4 * (lane >> 5)) * SROW + wn * 64 + nb * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * SROW] = acc[mb][nb][r];
+      });
+    });
+    __syncthreads();
+    // ---- row phase: output pixels j = pl, pl + PL, ... of this half
+#pragma unroll 2
+    for (int j = pl; j < NPO; j += PL) {
+      float4 v;
+      int y, x, g;
+      if constexpr (POOL) {
+        // staged pixel s = row*32 + col over rows 0/1 and columns [32h, 32h+32)
+        const float* s0 = stage + (2 * j) * SROW + cg * 4;
+        const float4 o00 = ld4(s0), o01 = ld4(s0 + SROW), o10 = ld4(s0 + 32 * SROW), o11 = ld4(s0 + 33 * SROW);
+        auto pool1 = [&](float a00, float a10, float a01, float a11, float bb) {
+          return ((((a00 + bb) + (a10 + bb)) + (a01 + bb)) + (a11 + bb)) / 4.0f;  // layers.py:310-312
+        };
+        v.x = pool1(o00.x, o10.x, o01.x, o11.x, bias4.x);
+        v.y = pool1(o00.y, o10.y, o01.y, o11.y, bias4.y);
+        v.z = pool1(o00.z, o10.z, o01.z, o11.z, bias4.z);
+        v.w = pool1(o00.w, o10.w, o01.w, o11.w, bias4.w);
+        y = (sr0 + wrow0) >> 1;
+        x = (sc0 + 32 * h + 2 * j) >> 1;
+        g = 0;
+      } else {
+        const float4 o = ld4(stage + j * SROW + cg * 4);
+        v = make_float4(o.x + bias4.x, o.y + bias4.y, o.z + bias4.z, o.w + bias4.w);
+        const int ws = j >> 6, q = j & 63;                 // staged pixel -> (wave row block, pixel)
+        const int mb = 2 * h + (q >> 5);
+        const int row = ws * T::RW + mb / (TC / 32), col = (mb % (TC / 32)) * 32 + (q & 31);
+        y = (sr0 + row) * d + ph_r;
+        x = (sc0 + col) * d + ph_c;
+        g = ws;
+      }
+      const size_t oidx = ((size_t)y * Wo + x) * Cout + co0;
       if (a.up) {
         // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor at (y, x)
         const int Hi = a.H / 2, Wi = a.W / 2;
@@ -399,69 +493,85 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         const int y0 = (int)fy, x0 = (int)fx;
         const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
         const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
-        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co;
-        const float v00 = ub[((size_t)y0 * Wi + x0) * Cout], v01 = ub[((size_t)y0 * Wi + x0 + xp) * Cout];
-        const float v10 = ub[((size_t)(y0 + yp) * Wi + x0) * Cout], v11 = ub[((size_t)(y0 + yp) * Wi + x0 + xp) * Cout];
-        v = v + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
+        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co0;
+        const float4 v00 = ld4(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = ld4(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
+        const float4 v10 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
+        const float4 v11 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
+        auto bil = [&](float a00, float a01, float a10, float a11) {
+          return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+        };
+        v.x = v.x + bil(v00.x, v01.x, v10.x, v11.x);
+        v.y = v.y + bil(v00.y, v01.y, v10.y, v11.y);
+        v.z = v.z + bil(v00.z, v01.z, v10.z, v11.z);
+        v.w = v.w + bil(v00.w, v01.w, v10.w, v11.w);
       }
-      if (a.res) v = a.res[oidx] + v;
-      if (a.out2) a.out2[oidx] = v + a.res2[oidx];
-      if (a.epi_elu) v = elu(v);
-      a.out[oidx] = v;
-      ++cnt;
-      const float delta = v - wmean[nb];
-      wmean[nb] = fmaf(delta, 1.0f / (float)cnt, wmean[nb]);
-      wm2[nb] = fmaf(delta, v - wmean[nb], wm2[nb]);
-    };
-    if constexpr (POOL) {
-      static_assert(TC == 64 && WM == 1, "pooling tiles: 2 rows x 64 columns per wave");
-      // frags mb (row 0) and mb+2 (row 1) hold vertically adjacent pixels; regs r, r+1 hold
-      // horizontally adjacent ones
-      static_for<0, 2>([&](auto mbc) {
-        constexpr int mb = decltype(mbc)::value;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int r = 2 * i;
-          const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          const float o00 = acc[mb][nb][r] + bias, o10 = acc[mb + 2][nb][r] + bias;
-          const float o01 = acc[mb][nb][r + 1] + bias, o11 = acc[mb + 2][nb][r + 1] + bias;
-          const float v = (((o00 + o10) + o01) + o11) / 4.0f;  // layers.py:310-312 summation order
-          emit(v, (sr0 + wrow0) >> 1, (sc0 + mb * 32 + m) >> 1);
-          if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-        }
-      });
-    } else {
-      static_for<0, 4>([&](auto mbc) {
-        constexpr int mb = decltype(mbc)::value;
-        constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          emit(acc[mb][nb][r] + bias, (sr0 + wrow0 + mr) * d + ph_r, (sc0 + mc + m) * d + ph_c);
-          // keep the compiler from hoisting every epilogue load at once
-          if ((r & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+      const size_t bo = (size_t)b * Ho * Wo * Cout;
+      if (a.res) {
+        const float4 r4 = ld4(a.res + bo + oidx);
+        v = make_float4(r4.x + v.x, r4.y + v.y, r4.z + v.z, r4.w + v.w);
+      }
+      if (a.out2) {
+        const float4 r4 = ld4(a.res2 + bo + oidx);
+        *reinterpret_cast<float4*>(a.out2 + bo + oidx) = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
+      }
+      if (a.epi_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
+      if constexpr (!(SDP_KO & 16)) *reinterpret_cast<float4*>(outb + oidx) = v;
+      static_for<0, WM>([&](auto gc) {
+        constexpr int gg = decltype(gc)::value;
+        if (gg == g) {
+          if (sn[gg] == 0) sK[gg] = v;
+          const float4 dv = make_float4(v.x - sK[gg].x, v.y - sK[gg].y, v.z - sK[gg].z, v.w - sK[gg].w);
+          s1[gg] = make_float4(s1[gg].x + dv.x, s1[gg].y + dv.y, s1[gg].z + dv.z, s1[gg].w + dv.w);
+          s2[gg] = make_float4(fmaf(dv.x, dv.x, s2[gg].x), fmaf(dv.y, dv.y, s2[gg].y), fmaf(dv.z, dv.z, s2[gg].z),
+                               fmaf(dv.w, dv.w, s2[gg].w));
+          ++sn[gg];
         }
       });
     }
+    __syncthreads();   // staging buffer reused by the next half / the statistics
   });
 
   if (a.stats) {
-    // per wave = one 128-pixel group: Chan merge of lanes l / l+32 (equal counts)
-    const int group = tile * WM + wm;
-    const float n = (float)cnt;
-    static_for<0, 2>([&](auto nbc) {
-      constexpr int nb = decltype(nbc)::value;
-      const float om = __shfl_xor(wmean[nb], 32), o2 = __shfl_xor(wm2[nb], 32);
-      const float dm = om - wmean[nb];
-      const float mean = 0.5f * (wmean[nb] + om);
-      const float m2 = wm2[nb] + o2 + dm * dm * (0.5f * n);
-      if (lane < 32) {
-        const int co = n0 + wn * 64 + nb * 32 + lane;
-        float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + group) * Cout + co;
-        *st = make_float2(mean, m2);
+    // per-thread partials -> (mean, M2) in LDS, then a Chan merge over the PL threads of a
+    // channel group; one 128-pixel statistics group per wave row block (WM)
+    float2* part = reinterpret_cast<float2*>(lds);   // [WM][PL][NTILE]
+    static_for<0, WM>([&](auto gc) {
+      constexpr int gg = decltype(gc)::value;
+      const float n = (float)sn[gg], inv = sn[gg] ? 1.f / n : 0.f;
+      const float k4[4] = {sK[gg].x, sK[gg].y, sK[gg].z, sK[gg].w};
+      const float a4[4] = {s1[gg].x, s1[gg].y, s1[gg].z, s1[gg].w};
+      const float q4[4] = {s2[gg].x, s2[gg].y, s2[gg].z, s2[gg].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float mean = k4[c] + a4[c] * inv;
+        const float m2 = fmaxf(q4[c] - a4[c] * a4[c] * inv, 0.f);
+        part[(gg * PL + pl) * T::NTILE + cg * 4 + c] = make_float2(mean, m2);
       }
     });
+    __syncthreads();
+    constexpr int PER = (POOL ? 32 : 128) / PL;      // values per thread per statistics group
+    for (int i = tid; i < WM * T::NTILE; i += 256) {
+      const int gg = i / T::NTILE, co = i % T::NTILE;
+      float mean = 0.f;
+      for (int k = 0; k < PL; ++k) mean += part[(gg * PL + k) * T::NTILE + co].x;
+      mean *= 1.f / PL;
+      float m2 = 0.f;
+      for (int k = 0; k < PL; ++k) {
+        const float2 pk = part[(gg * PL + k) * T::NTILE + co];
+        const float dm = pk.x - mean;
+        m2 += pk.y + (float)PER * dm * dm;
+      }
+      float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile * WM + gg) * Cout + n0 + co;
+      *st = make_float2(mean, m2);
+    }
   }
+#ifdef SDP_TIMING
+  SDP_T(4);
+  if (tid == 0) {
+    unsigned long long* o = a.dbg + blockIdx.x * 8;
+    o[0] = tclk[0]; o[1] = tclk[1]; o[2] = tclk[2]; o[3] = tclk[3]; o[4] = tclk[4]; o[5] = tbar;
+  }
+#endif
 #endif
 }
 
@@ -486,8 +596,13 @@ static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int t
 
 template <int MODE>
 static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
+#ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
+  if (wm == 2) return launch_t<MODE, 2, 32, 3, false, true>(a, st);
+  return launch_t<MODE, 1, 64, 3, false, true>(a, st);
+#else
   return a.pro_mode == PRO_NONE ? launch_elu<MODE, false>(a, ks, pool, wm, tc, st)
                                 : launch_elu<MODE, true>(a, ks, pool, wm, tc, st);
+#endif
 }
 
 // Host entry: validates the shape contract the kernel's indexing assumes, then launches.
@@ -509,8 +624,11 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   }
   if (a.up && ((a.H & 1) || (a.W & 1) || a.H < 2 || a.W < 2)) { *why = "conv: upsample needs even H,W"; return hipErrorInvalidValue; }
   if (!a.circular && d != 1) { *why = "conv: zero padding only for d=1"; return hipErrorInvalidValue; }
-  if (a.pro_mode == PRO_AFFINE_ELU && !a.pro_ss) { *why = "conv: affine prologue without scale/shift"; return hipErrorInvalidValue; }
-  if (a.pro_mode != PRO_AFFINE_ELU) a.pro_ss = nullptr;
+  if (!a.pro_ss) { *why = "conv: prologue scale/shift table missing"; return hipErrorInvalidValue; }
+  if (a.Cin > 1024 && a.ss_bstride == 0) { *why = "conv: identity table holds 1024 channels"; return hipErrorInvalidValue; }
+#ifdef SDP_CONV_BENCH_ONLY
+  return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
+#endif
   switch (mode) {
     case MODE_F32: return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
     case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);

@@ -162,7 +162,8 @@ struct Fwd {
     a.out2 = o.out2;
     a.res2 = o.res2;
     a.up = o.up;
-    a.pro_ss = o.pro == PRO_AFFINE_ELU ? ss : nullptr;
+    a.pro_ss = o.pro == PRO_AFFINE_ELU ? ss : net->P("#ident_ss");
+    a.ss_bstride = o.pro == PRO_AFFINE_ELU ? 2 * in.C : 0;
     a.stats = o.stats ? stats : nullptr;
     a.B = B;
     a.H = in.H;
@@ -439,6 +440,10 @@ int sdp_net_finalize(sdp_net* net) {
         upload(k + "#frag", fr.data(), fr.size() * 4);
       }
     }
+    // identity (scale, shift) = (1, 0) rows for convs without an InstanceNorm++ prologue
+    std::vector<float> ident(2 * 1024);
+    for (size_t i = 0; i < ident.size(); i += 2) ident[i] = 1.f;
+    upload("#ident_ss", ident.data(), ident.size() * 4);
     net->finalized = true;
   } catch (const std::exception& e) {
     return fail(std::string("sdp_net_finalize: ") + e.what());

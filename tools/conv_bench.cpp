@@ -1,0 +1,74 @@
+// Standalone timing of one conv_mfma launch shape (diagnostics; links a conv.o built with
+// -DSDP_CONV_BENCH_ONLY [-DSDP_KO=mask]).  Usage: conv_bench Cin Cout H W B [dil] [iters]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../simultaneous-diffusion-for-pointclouds_amd/csrc/kernels.h"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+int main(int argc, char** argv) {
+  const int Cin = atoi(argv[1]), Cout = atoi(argv[2]), H = atoi(argv[3]), W = atoi(argv[4]), B = atoi(argv[5]);
+  const int dil = argc > 6 ? atoi(argv[6]) : 1, iters = argc > 7 ? atoi(argv[7]) : 20;
+  const size_t nin = (size_t)B * H * W * Cin, nout = (size_t)B * H * W * Cout, nw = (size_t)Cout * Cin * 9;
+  std::vector<float> h(std::max(nin, nw));
+  srand(1);
+  for (auto& v : h) v = (float)rand() / RAND_MAX - 0.5f;
+  float *in, *out, *ss, *stats, *bias;
+  uint32_t* wf;
+  CK(hipMalloc(&in, nin * 4));
+  CK(hipMalloc(&out, nout * 4));
+  CK(hipMalloc(&wf, nw * 4));
+  CK(hipMalloc(&ss, (size_t)B * Cin * 2 * 4));
+  CK(hipMalloc(&stats, (size_t)B * (H * W / 128) * Cout * 2 * 4));
+  CK(hipMalloc(&bias, Cout * 4));
+  CK(hipMemcpy(in, h.data(), nin * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(wf, h.data(), nw * 4, hipMemcpyHostToDevice));   // random bits: timing only
+  std::vector<float> sh((size_t)B * Cin * 2);
+  for (size_t i = 0; i < sh.size(); i += 2) { sh[i] = 1.f; sh[i + 1] = 0.f; }
+  CK(hipMemcpy(ss, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(bias, 0, Cout * 4));
+  sdp::ConvArgs a{};
+  a.in = in; a.wf = reinterpret_cast<const uint4*>(wf); a.bias = bias; a.out = out; a.pro_ss = ss;
+  a.ss_bstride = 2 * Cin; a.stats = stats; a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
+  a.dil = dil; a.circular = 1; a.pro_mode = sdp::PRO_AFFINE_ELU; a.epi_elu = 0;
+  unsigned long long* dbg;
+  const int nwg_max = B * H * W / 128;
+  CK(hipMalloc(&dbg, (size_t)nwg_max * 8 * 8));
+  CK(hipMemset(dbg, 0, (size_t)nwg_max * 8 * 8));
+  a.dbg = dbg;
+  const char* why = "";
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int i = 0; i < 3; ++i) CK(sdp::conv_mfma(sdp::MODE_F32X3, a, 3, false, 0, &why));
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(sdp::conv_mfma(sdp::MODE_F32X3, a, 3, false, 0, &why));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double us = ms * 1e3 / iters, fl = 2.0 * B * H * W * (double)Cin * Cout * 9;
+  printf("conv %d->%d @%dx%d B=%d d=%d: %.1f us  %.1f TF/s (fp32x3 algorithmic)\n", Cin, Cout, H, W, B, dil, us,
+         fl / us * 1e-6);
+#ifdef SDP_TIMING
+  std::vector<unsigned long long> d((size_t)nwg_max * 8);
+  CK(hipMemcpy(d.data(), dbg, d.size() * 8, hipMemcpyDeviceToHost));
+  double s[6] = {0}; int n = 0; unsigned long long tmin = ~0ull, tmax = 0;
+  for (int i = 0; i < nwg_max; ++i) {
+    const unsigned long long* o = &d[(size_t)i * 8];
+    if (!o[0]) continue;
+    ++n;
+    s[0] += o[1] - o[0]; s[1] += o[2] - o[1]; s[2] += o[3] - o[2]; s[3] += o[4] - o[3]; s[4] += o[5];
+    s[5] += o[4] - o[0];
+    tmin = std::min(tmin, o[0]); tmax = std::max(tmax, o[4]);
+  }
+  printf("  per-WG memtime ticks (n=%d): setup %.0f  prologue %.0f  loop %.0f (barrier %.0f)  epilogue %.0f  total %.0f ; "
+         "span of last launch %llu\n", n, s[0] / n, s[1] / n, s[2] / n, s[4] / n, s[3] / n, s[5] / n, tmax - tmin);
+#endif
+  return 0;
+}

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Build conv_bench variants (knock-out masks) here; run them on the GPU with RUN=1.
+set -eu
+cd "$(dirname "$0")/.."
+mkdir -p tools/_cb
+SRC=simultaneous-diffusion-for-pointclouds_amd/csrc
+if [ "${RUN:-0}" = 0 ]; then
+  for ko in ${KOS:-0 1 2 4 8 16}; do
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize -DSDP_CONV_BENCH_ONLY -DSDP_KO=$ko ${EXTRA:-} \
+      -c $SRC/conv.hip -o tools/_cb/conv_$ko.o &
+  done
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 ${EXTRA:-} -c tools/conv_bench.cpp -o tools/_cb/main.o
+  for ko in ${KOS:-0 1 2 4 8 16}; do
+    /opt/rocm/bin/hipcc --offload-arch=gfx950 tools/_cb/main.o tools/_cb/conv_$ko.o -o tools/_cb/conv_bench_$ko
+  done
+else
+  for ko in ${KOS:-0 1 2 4 8 16}; do
+    echo "KO=$ko"
+    timeout -k 5 60 tools/_cb/conv_bench_$ko 256 256 32 512 4 1 20
+    timeout -k 5 60 tools/_cb/conv_bench_$ko 128 128 64 1024 4 1 20
+  done
+fi
