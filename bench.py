@@ -74,6 +74,24 @@ def cpu_baseline(V, H, W, threads):
                       f"(torch CPU fp32 + numpy), {dt:.2f} s"}
 
 
+def pmc_traffic(precision, V):
+    """HBM bytes per launch of the dominant conv class from the committed PMC passes
+    (tools/pmc_traffic.sh -> profiles/r01_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
+    correction) + TCC_EA0_WRREQ bytes, averaged over that kernel's launches at this grid)."""
+    mode = {"fp32": 0, "fp32x3": 1, "bf16": 2}[precision]
+    name = f"void sdp::conv_mfma_kernel<{mode}, 1, 64, 3, false, true>(sdp::ConvArgs)"
+    grid = V * (32 * 512 // 128) * 256
+    try:
+        with open(os.path.join(REPO, "profiles", "r01_traffic.json")) as f:
+            rows = json.load(f)
+    except OSError:
+        return None
+    for r in rows:
+        if r["kernel"] == name and r["grid"] == grid and "hbm_bytes" in r:
+            return round(r["hbm_bytes"])
+    return None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -163,7 +181,9 @@ def main():
         achieved = fl / avg_s / 1e12
         conv_ms = sum(v[1] for v in prof.values()) / args.steps
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[args.precision], 1),
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4),
+                "traffic": pmc_traffic(args.precision, V), "traffic_unit": "bytes/launch (PMC, profiles/r01_traffic.json)",
+                "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if args.precision == "bf16" else 4),
                 "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
                 "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3)}
         cpu = None

@@ -14,12 +14,13 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d $OUT/p$i -o run --output-format csv -- \
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $grp -d $OUT/p$i -o run --output-format csv -- \
     python bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc: $grp"
   if [ $rc -ne 0 ]; then tail -5 $OUT/p$i.log; exit $rc; fi
 done <<'GROUPS'
 TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
-FETCH_SIZE WRITE_SIZE
+FETCH_SIZE
+WRITE_SIZE
 GROUPS
-python tools/pmc_traffic.py $OUT profiles/${ROUND}_traffic.json
+python tools/pmc_traffic.py $OUT $OUT/${ROUND}_traffic.json
