@@ -15,6 +15,10 @@
  *                                                                     models/__init__.py:236-259, :1397-1416
  *   sdp_consistency_merge  cross-view reprojection + correction      models/KITTISampling.py:160-490 (pose matrices),
  *                                                                     models/__init__.py:263-579 (origin offsets)
+ *   sdp_net_forward_train  scores = scorenet(perturbed, labels) in train mode   losses/dsm.py:85
+ *   sdp_dsm_loss           anneal_dsm_score_estimation_with_mask            losses/dsm.py:67-119
+ *   sdp_net_backward       loss.backward()                                  runners/ncsn_runner_kitti_simultaneous.py:230
+ *   sdp_adam_ema_step      optimizer.step() (Adam, losses/__init__.py:10-20) + EMAHelper.update (models/ema.py:16-21)
  */
 #ifndef SDP_H
 #define SDP_H
@@ -65,6 +69,41 @@ int sdp_net_destroy(sdp_net* net);
  * line per conv class: "class\tlaunches\ttotal_ms\tflops_per_launch\n". */
 int sdp_net_profile_enable(sdp_net* net, int enable);
 int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches);
+
+/* ---- parameters as one device arena (training) ------------------------------------------
+ * Every learnable parameter (state_dict keys minus the "sigmas" buffer), float32, in key order,
+ * each at a 64-float aligned offset.  sdp_net_bind_params copies the current values into a
+ * caller-owned device arena of sdp_net_param_arena_floats floats and makes it the net's
+ * parameter storage; after the caller changes it (optimizer), sdp_net_repack rebuilds the
+ * packed conv weights on `stream`.  Gradient arenas use the same layout.                    */
+int sdp_net_param_arena_floats(const sdp_net* net, size_t* n);
+int sdp_net_param_count(const sdp_net* net, int* n);
+int sdp_net_param_info(const sdp_net* net, int i, char* key, size_t cap, size_t* offset, size_t* numel);
+int sdp_net_bind_params(sdp_net* net, float* arena, void* stream);
+int sdp_net_repack(sdp_net* net, void* stream);
+
+/* ---- DSM training (BASELINE config 5; precision fp32x3 or bf16) -------------------------
+ * sdp_net_forward_train: out = scorenet(x, labels), keeping every tensor the backward needs
+ * (the tape) in `workspace` (sdp_net_train_workspace_size bytes).  sdp_net_backward then writes
+ * d loss/d parameters for d loss/d out = dscore into `grads` (a parameter-layout arena,
+ * overwritten) -- same workspace and B, no other train-mode call on this net in between.   */
+int sdp_net_train_workspace_size(sdp_net* net, int B, size_t* bytes);
+int sdp_net_forward_train(sdp_net* net, const float* x, const int64_t* labels, float* out, int B,
+                          void* workspace, size_t workspace_bytes, void* stream);
+int sdp_net_backward(sdp_net* net, const float* dscore, int B, void* workspace, size_t workspace_bytes,
+                     float* grads, void* stream);
+/* loss = mean_b 1/2 * sum_i (mask*(score - target))^2 * n_img / sum(mask) * sigma_b^p with
+ * target = -noise / sigma_b^2 (noise already scaled by sigma_b, as the reference passes it);
+ * writes dscore = d loss / d score, loss[0], loss_per[b] (optional).  mask float32 0/1,
+ * n_img = C*H*W, part: 2*B*64 floats of scratch.                                             */
+int sdp_dsm_loss(const float* score, const float* noise, const float* mask, const float* used_sigma, int B,
+                 int n_img, float anneal_power, float* dscore, float* loss, float* loss_per, float* part,
+                 void* stream);
+/* torch.optim.Adam step (weight_decay 0, amsgrad off) over n floats, step = 1, 2, ...; then
+ * ema_shadow = (1 - ema_mu)*p + ema_mu*ema_shadow if ema_shadow is not NULL.                 */
+int sdp_adam_ema_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema_shadow,
+                      size_t n, float lr, float beta1, float beta2, float eps, int step, float ema_mu,
+                      void* stream);
 
 /* ---- Langevin update ------------------------------------------------------------------ *
  * x <- x + step*g' + grad_ref*lik + noise*noise_scale   (float32, reference evaluation order)

@@ -151,3 +151,28 @@ def scorenet_forward(P, x, y, ngf=128):
 
 def to_torch_params(sd):
     return {k: torch.as_tensor(v) for k, v in sd.items()}
+
+
+def dsm_loss(scores, used_sigmas, noise, masks, anneal_power=2.0):
+    """Loss of anneal_dsm_score_estimation_with_mask with used_sigmas given (losses/dsm.py:80-93)."""
+    B = scores.shape[0]
+    target = -1 / (used_sigmas ** 2) * noise
+    masks = masks.reshape(B, -1)
+    target = target.reshape(B, -1)
+    s = scores.reshape(B, -1)
+    num_pixels = masks.sum()
+    loss = 1 / 2. * (((masks * (s - target)) ** 2).sum(dim=-1) * masks.shape[-1] / num_pixels) \
+        * used_sigmas.squeeze() ** anneal_power
+    return loss.mean(dim=0)
+
+
+def dsm_loss_and_grads(P, X, noise, masks, labels, anneal_power=2.0):
+    """(loss, scores, {key: d loss/d param}) by autograd through scorenet_forward (the
+    reference's loss.backward(), runners/ncsn_runner_kitti_simultaneous.py:230)."""
+    Q = {k: (v.clone().requires_grad_(k != "sigmas")) for k, v in P.items()}
+    used = Q["sigmas"].detach()[labels].view(X.shape[0], 1, 1, 1)
+    scores = scorenet_forward(Q, X, labels)
+    loss = dsm_loss(scores, used, noise, masks, anneal_power)
+    loss.backward()
+    grads = {k: v.grad for k, v in Q.items() if k != "sigmas"}
+    return loss.detach(), scores.detach(), grads

@@ -139,7 +139,8 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
 __global__ __launch_bounds__(1024) void inpp_finalize_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
                                                              const float* __restrict__ alpha,
                                                              const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta, float2* __restrict__ ss) {
+                                                             const float* __restrict__ beta, float2* __restrict__ ss,
+                                                             float4* __restrict__ nst) {
   __shared__ double red[1024];
   const int b = blockIdx.x, tid = threadIdx.x;
   const int G = blockDim.x / C, g = tid / C, c = tid % C;
@@ -192,6 +193,8 @@ __global__ __launch_bounds__(1024) void inpp_finalize_kernel(const float2* __res
   const double scale = gm * inv;
   const double shift = gm * (-mean * inv + mn * (double)alpha[c]) + (double)beta[c];
   ss[(size_t)b * C + c] = make_float2((float)scale, (float)shift);
+  // training: the per-(b,c) statistics the backward needs (mean, rstd, mhat, 1/sqrt(v + eps))
+  if (nst) nst[(size_t)b * C + c] = make_float4((float)mean, (float)inv, (float)mn, (float)(1.0 / sqrt(v + 1e-5)));
 }
 
 // ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
@@ -236,9 +239,9 @@ hipError_t end_conv(const float* in, const float* ss, const float* w, const floa
 }
 
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
-                         const float* beta, float* ss, hipStream_t st) {
+                         const float* beta, float* ss, hipStream_t st, float* nst) {
   hipLaunchKernelGGL(inpp_finalize_kernel, dim3(B), dim3(1024), 0, st, reinterpret_cast<const float2*>(stats), T, cnt, C,
-                     alpha, gamma, beta, reinterpret_cast<float2*>(ss));
+                     alpha, gamma, beta, reinterpret_cast<float2*>(ss), reinterpret_cast<float4*>(nst));
   return hipGetLastError();
 }
 

@@ -31,6 +31,11 @@ SDP_DEV float elu(float x) { return x > 0.f ? x : (__expf(x) - 1.0f); }
 // the same values without a compare/select (e^x - 1 >= x, and e^min(x,0) - 1 = 0 for x > 0):
 // no VCC round trip, so it schedules freely between MFMAs
 SDP_DEV float elu_max(float x) { return fmaxf(x, __expf(fminf(x, 0.f)) - 1.0f); }
+// d ELU / d h, from the pre-activation h (form 1, 3) or from the output y = ELU(h) (form 2)
+SDP_DEV float elu_grad(float t, int form) {
+  if (form == 2) return t > 0.f ? 1.f : t + 1.f;
+  return t > 0.f ? 1.f : __expf(t);
+}
 
 // Arguments of one implicit-GEMM 3x3 / 1x1 convolution launch (activations NHWC float32).
 struct ConvArgs {
@@ -51,6 +56,24 @@ struct ConvArgs {
   int tiles_per_img;       // workgroup tiles per image (set by the launcher)
   int groups_per_img;      // 128-pixel statistics groups per image (H*W/128)
   unsigned long long* dbg; // diagnostics builds only (SDP_TIMING): per-workgroup phase clocks
+  // backward epilogue (data gradient): out *= elu'(...) of `aux` (layout of out) before +res;
+  // dact 0 = off, 1 = aux is the pre-activation, 2 = aux is the ELU output, 3 = aux is the
+  // InstanceNorm++ input and epi_ss [B][Cout][2] its (scale, shift)
+  const float* aux;
+  const float* epi_ss;
+  int dact;
+};
+
+// Arguments of one weight-gradient launch (wgrad.hip).
+struct WgradArgs {
+  const float* in;         // forward input [B][H][W][Cin] (before the prologue)
+  const float* pro_ss;     // prologue (scale, shift) table, as ConvArgs
+  int ss_bstride;
+  int pro_mode;            // PRO_NONE / PRO_ELU / PRO_AFFINE_ELU
+  const float* dy;         // gradient of the conv output (before any pooling) [B][H][W][Cout]
+  float* part;             // split partials [S][k*k][Cout][Cin]
+  size_t part_floats;
+  int B, H, W, Cin, Cout, dil, circular;
 };
 
 }  // namespace sdp

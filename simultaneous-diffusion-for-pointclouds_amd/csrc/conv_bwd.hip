@@ -1,0 +1,54 @@
+// Data gradient of the score network's convolutions (DSM training, LiDARGen/losses/dsm.py:67-119
+// through NCSN_LiDAR_small).  A stride-1 conv with circular or zero padding is adjoint to the
+// same conv over the output gradient with the kernel flipped in both taps and transposed in
+// (Cin, Cout) -- circular padding stays circular, zero padding stays zero, a dilation stays
+// the same dilation -- so the data gradient is the forward implicit-GEMM kernel
+// (conv_kernel.h) run on dy with the "dgrad" weight packing (train_aux.hip pack kernel),
+// without prologue, and with the backward epilogue: *elu'(...) of the forward activation
+// (ConvArgs::dact) and the residual add of the gradient already accumulated for its input.
+#include "conv_kernel.h"
+
+namespace sdp {
+
+template <int MODE, int WM, int TC, int KS, bool ZP>
+static hipError_t launch_dgrad_t(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<WM, TC, KS>;
+  a.tiles_per_img = a.H * a.W / (T::TR * TC);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, hipStream_t st) {
+  if (ks == 1) return launch_dgrad_t<MODE, 2, 32, 1, false>(a, st);
+  if (!a.circular) return launch_dgrad_t<MODE, 2, 32, 3, true>(a, st);
+  if (wm == 2) return launch_dgrad_t<MODE, 2, 32, 3, false>(a, st);
+  return tc == 64 ? launch_dgrad_t<MODE, 1, 64, 3, false>(a, st) : launch_dgrad_t<MODE, 1, 32, 3, false>(a, st);
+}
+
+// a.in = dy [B][H][W][Cin = forward Cout], a.wf = dgrad-packed weights, a.out = dx
+// [B][H][W][Cout = forward Cin].  Same shape contract as conv_mfma, no pooling, no prologue.
+hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char** why) {
+  const int d = a.dil;
+  if (a.Cin % 64 || a.Cout % 128) { *why = "dgrad: Cin%64 and Cout%128 required"; return hipErrorInvalidValue; }
+  if (a.H % d || a.W % d) { *why = "dgrad: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
+  if (a.pro_mode != PRO_NONE || a.up || a.out2 || a.stats) { *why = "dgrad: plain input, no fused extras"; return hipErrorInvalidValue; }
+  const int Hs = a.H / d, Ws = a.W / d;
+  const int wm = (a.Cout % 256 == 0 && ks == 3 && a.circular) ? 1 : 2;
+  const int tc = (wm == 2) ? 32 : ((Ws % 64 == 0) ? 64 : 32);
+  const int tr = wm * 128 / tc;
+  if (Ws % tc || Hs % tr) { *why = "dgrad: sub-grid not divisible by the pixel tile"; return hipErrorInvalidValue; }
+  if (!a.circular && d != 1) { *why = "dgrad: zero padding only for d=1"; return hipErrorInvalidValue; }
+  if (a.dact && !a.aux) { *why = "dgrad: dact needs aux"; return hipErrorInvalidValue; }
+  if (a.dact == 3 && !a.epi_ss) { *why = "dgrad: dact 3 needs epi_ss"; return hipErrorInvalidValue; }
+  if (!a.pro_ss) { *why = "dgrad: prologue identity table missing"; return hipErrorInvalidValue; }
+  switch (mode) {
+    case MODE_F32X3: return launch_dgrad_mode<MODE_F32X3>(a, ks, wm, tc, st);
+    case MODE_BF16: return launch_dgrad_mode<MODE_BF16>(a, ks, wm, tc, st);
+    default: *why = "dgrad: training runs in fp32x3 or bf16"; return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace sdp

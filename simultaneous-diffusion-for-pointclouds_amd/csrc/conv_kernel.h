@@ -1,0 +1,592 @@
+// Implicit-GEMM convolution kernel on MFMA for the NCSN/RefineNet score network (gfx950).
+//
+// Covers every 3x3 conv of NCSN_LiDAR_small except begin/end conv:
+//   conv3x3 circular (LiDARGen/models/layers.py:37-44), dilated_conv3x3 circular
+//   (layers.py:55-60), ConvMeanPool 3x3/1x1 zero-pad + 2x2 mean (layers.py:291-313).
+//
+// GEMM view: M = output pixels, N = Cout, K = taps x Cin.  One workgroup = 4 waves, ONE wave
+// per SIMD (512-register budget, accumulators in AGPRs); each wave owns 128 px x 64 Cout =
+// 4 x 2 blocks of the 32x32 MFMA tile, so per (tap, 16-wide k step) it reads 8 A fragments
+// from LDS and 4 B fragments from L2 for 24 MFMAs (fp32x3).  Workgroup shapes:
+//   WM=1: 128 px x 256 Cout (4 waves side by side in N; the patch serves 256 channels)
+//   WM=2: 256 px x 128 Cout (2 x 2 waves; for the 128-channel layers)
+// Dilated convs run on their d x d polyphase sub-grids, so a tile is always TR x TC pixels
+// of one sub-grid and its input patch has a 1-pixel halo whatever d.
+//
+// K loop, per 32-channel chunk, fully software-pipelined (one barrier per chunk):
+//   raw   : the fp32 (TR+2) x (TC+2) x 32 input patch of chunk k+1, landed by LDS-DMA
+//           (buffer_load ... lds) during chunk k-1
+//   patch : two buffers; while the 9 taps of chunk k run their MFMAs on patch[k&1], the
+//           taps 0..3 transform raw -> patch[(k+1)&1] (consumer prologue: InstanceNorm++
+//           affine and/or ELU, zero padding, bf16 hi/lo split) and the taps 4..8 issue the
+//           LDS-DMA of chunk k+2 into raw.
+//   weights: pre-arranged on the host in MFMA fragment order, streamed from L2 into VGPRs
+//           one tap ahead (buffer_load_b128 with a scalar per-(chunk, tap) offset).
+//
+// MODE_F32   : v_mfma_f32_32x32x2_f32 on fp32 operands (exact fp32 products).
+// MODE_F32X3 : operands split x = hi + lo (bf16 each), acc += hi*hi + hi*lo + lo*hi on
+//              v_mfma_f32_32x32x16_bf16 -- error ~2e-5 of max|out| on the full network.
+// MODE_BF16  : hi*hi only.
+//
+// Epilogue (fused): +bias, 2x2 mean-pool, +residual, +bilinear upsample of a half-res
+// tensor, ELU, a second output (value + res2), and per-128-pixel InstanceNorm++ statistics
+// (mean, M2) of every output channel.
+#pragma once
+#include <type_traits>
+
+#include "common.h"
+
+namespace sdp {
+
+// Diagnostic knock-outs for tools/conv_bench (never set in the library build):
+// 1 = no patch DMA, 2 = no transform, 4 = no weight loads, 8 = no chunk barrier, 16 = no epilogue
+#ifndef SDP_KO
+#define SDP_KO 0
+#endif
+
+#ifdef SDP_TIMING   // tools/conv_bench: per-workgroup phase clocks of wave 0 into a.dbg
+#define SDP_T(i) do { if (tid == 0) tclk[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define SDP_T(i) do { } while (0)
+#endif
+
+constexpr int PSTRIDE = 144;  // bytes per staged patch pixel: 32 ch x (hi,lo bf16) or 32 x f32, + 16 pad
+
+template <int WM, int TC, int KS>
+struct ConvTile {
+  static constexpr int WN = 4 / WM;                // waves along N
+  static constexpr int RW = 128 / TC;              // pixel rows per wave
+  static constexpr int TR = WM * RW;               // tile rows
+  static constexpr int NTILE = WN * 64;            // output channels per workgroup
+  static constexpr int HALO = KS == 3 ? 1 : 0;
+  static constexpr int PC = TC + 2 * HALO;
+  static constexpr int PR = TR + 2 * HALO;
+  static constexpr int NPIX = PR * PC;
+  static constexpr int NU = (NPIX * 8 + 255) / 256;            // 16-B staging units per thread per chunk
+  static constexpr int PATCH_BYTES = NU * 32 * PSTRIDE;         // one transformed patch (+ slack: every
+                                                                //   staging unit has a pixel slot)
+  static constexpr int RAW_BYTES = NU * 256 * 16;               // raw fp32 patch landed by LDS-DMA
+  static constexpr int PIPE_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
+  static constexpr int EPI_BYTES = WM * 64 * (NTILE + 8) * 4;   // epilogue staging (one half)
+  static constexpr int LDS_BYTES = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+};
+
+SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU>
+__global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
+  using T = ConvTile<WM, TC, KS>;
+  constexpr int NT = KS * KS;
+  constexpr int NU = T::NU;
+  constexpr int XT = NT >= 4 ? 4 : NT;            // taps that carry the transform of the next chunk
+  __shared__ __attribute__((aligned(16))) char lds[T::LDS_BYTES];
+  char* const raw = lds + 2 * T::PATCH_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef SDP_TIMING
+  unsigned long long tclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tbar = 0;
+#endif
+  SDP_T(0);
+  const int wm = WM == 1 ? 0 : (wave & 1), wn = WM == 1 ? wave : (wave >> 1);
+  const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
+  const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so give each XCD a
+  // contiguous range of tiles -- vertically adjacent tiles share their halo rows in its L2
+  const int nwg = gridDim.x;
+  int t = (nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3);
+  const int b = t / a.tiles_per_img;
+  const int tile = t - b * a.tiles_per_img;
+  t = tile;
+  const int ph = t / tiles_rc;
+  t -= ph * tiles_rc;
+  const int ph_r = ph / d, ph_c = ph - (ph / d) * d;
+  const int sr0 = (t / tiles_c) * T::TR, sc0 = (t % tiles_c) * TC;
+  const int n0 = blockIdx.y * T::NTILE;
+  const int wrow0 = wm * T::RW;                    // wave's first tile row
+
+  const int Cin = a.Cin, Cout = a.Cout;
+  const int nchunks = Cin / 32;
+  const int NB = Cout / 32;
+  const int nbg0 = n0 / 32 + wn * 2;               // global 32-channel block of this wave's nb=0
+
+  f32x16 acc[4][2];
+  static_for<0, 4>([&](auto i) {
+    static_for<0, 2>([&](auto j) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    });
+  });
+
+  // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
+  // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wf, 0, 0x7fffffff, 0x00020000);
+  const int wv0 = ((nbg0 + 0) * 64 + lane) * 64, wv1 = ((nbg0 + 1) * 64 + lane) * 64;
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  // weight fragment ring: 3 taps deep (prefetch distance 2) when the tap count is a multiple
+  // of 3, so the slot of (chunk, tap) is tap % 3 in every chunk; 2 deep for the 1x1 conv
+  constexpr int NBUF = (NT % 3 == 0) ? 3 : 2;
+  uint4 bq[NBUF][2][4];
+  auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
+    constexpr int J = decltype(buf)::value;
+    if constexpr (SDP_KO & 4) return;
+    const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096);
+    static_for<0, 4>([&](auto q) {
+      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
+      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
+      bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+      bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+    });
+  };
+
+  const float* inb = a.in + (size_t)b * a.H * a.W * Cin;
+  // (scale, shift) rows of this image (the identity table when there is no affine prologue):
+  // consumed only by the next chunk's transform, so the loads stay in flight across a chunk
+  const float* ssb = a.pro_ss + (size_t)b * a.ss_bstride;
+  const int my_cv = tid & 7;                        // every unit of a thread has cv == tid % 8
+  const int a_lane_off = (lane & 31) * PSTRIDE + (lane >> 5) * 16;
+  float4 ssv0, ssv1;                                // (scale, shift) of this thread's 4 channels
+  auto load_ss = [&](int chunk) __attribute__((always_inline)) {
+    ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
+    ssv1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
+  };
+
+  // Staging unit u = 16 B (4 channels) of one patch pixel.  Its byte offset inside the image
+  // (clamped into range, so every load is unconditional) and its validity (zero padding)
+  // depend only on the tile, so they are computed once; per chunk only the scalar channel
+  // offset changes.  Unit u is landed by lane u%64 of wave (u%256)/64 -- the same thread
+  // that transforms it, so raw needs no barrier, only the DMA's vmcnt.
+  // num_records = the image's bytes: the (unconditional) DMA of a chunk past the last one
+  // reads zeros instead of running off the tensor
+  const __amdgpu_buffer_rsrc_t irs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, a.H * a.W * Cin * 4, 0x00020000);
+  int uoff[NU];
+  unsigned uvalid = 0;
+  static_for<0, NU>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    int u = tid + k * 256;
+    bool valid = u < T::NPIX * 8;
+    u = valid ? u : 0;
+    const int pix = u >> 3, cv = u & 7;
+    const int pr = pix / T::PC, pc = pix - pr * T::PC;
+    int sr = sr0 - T::HALO + pr, sc = sc0 - T::HALO + pc;
+    if (a.circular) {
+      sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
+      sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
+    } else {
+      valid = valid && sr >= 0 && sr < Hs && sc >= 0 && sc < Ws;
+      sr = min(max(sr, 0), Hs - 1);
+      sc = min(max(sc, 0), Ws - 1);
+    }
+    const int y = sr * d + ph_r, x = sc * d + ph_c;
+    uoff[k] = ((y * a.W + x) * Cin + cv * 4) * 4;   // bytes, < 2^31 for every admitted shape
+    uvalid |= (valid ? 1u : 0u) << k;
+  });
+  // LDS-DMA of staging unit k: lane i of a wave lands 16 B at the wave-uniform base + 16*i
+  auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (SDP_KO & 1) return;
+    const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
+        uoff[k], chunk * 128, 0, 0);
+  };
+  // transform staging unit k of raw into patch buffer PB
+  // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
+  auto xform_load = [&](auto kc) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    return *reinterpret_cast<const float4*>(raw + (tid + k * 256) * 16);
+  };
+  auto xform_store = [&](auto kc, auto pb, float4 v) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    constexpr int PB = decltype(pb)::value;
+    const int pix = (tid + k * 256) >> 3;   // units past the patch land in its slack: no branch
+    v.x = fmaf(v.x, ssv0.x, ssv0.y);
+    v.y = fmaf(v.y, ssv0.z, ssv0.w);
+    v.z = fmaf(v.z, ssv1.x, ssv1.y);
+    v.w = fmaf(v.w, ssv1.z, ssv1.w);
+    if constexpr (PELU) {
+      v.x = elu_max(v.x); v.y = elu_max(v.y); v.z = elu_max(v.z); v.w = elu_max(v.w);
+    }
+    if constexpr (ZP) {   // zero padding (ConvMeanPool, layers.py:291-313, and its data gradient)
+      if (!((uvalid >> k) & 1u)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE;
+    if constexpr (MODE == MODE_F32) {
+      *reinterpret_cast<float4*>(dst + my_cv * 16) = v;
+    } else {
+      bf16x4 hi;
+      hi[0] = (__bf16)v.x; hi[1] = (__bf16)v.y; hi[2] = (__bf16)v.z; hi[3] = (__bf16)v.w;
+      *reinterpret_cast<bf16x4*>(dst + my_cv * 8) = hi;
+      if constexpr (MODE == MODE_F32X3) {
+        bf16x4 lo;
+        lo[0] = (__bf16)(v.x - (float)hi[0]);
+        lo[1] = (__bf16)(v.y - (float)hi[1]);
+        lo[2] = (__bf16)(v.z - (float)hi[2]);
+        lo[3] = (__bf16)(v.w - (float)hi[3]);
+        *reinterpret_cast<bf16x4*>(dst + 64 + my_cv * 8) = lo;
+      }
+    }
+  };
+  auto xform_unit = [&](auto kc, auto pb) __attribute__((always_inline)) { xform_store(kc, pb, xform_load(kc)); };
+  // half of unit k (channels 2h, 2h+1 of its 4): prologue + bf16 hi/lo split + one ds_write2
+  auto xform_piece = [&](auto kc, auto hc, auto pb, float4 v4) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value, h = decltype(hc)::value, PB = decltype(pb)::value;
+    if constexpr (SDP_KO & 2) return;
+    const int pix = (tid + k * 256) >> 3;
+    float x0 = h ? v4.z : v4.x, x1 = h ? v4.w : v4.y;
+    const float4 sv = h ? ssv1 : ssv0;
+    x0 = fmaf(x0, sv.x, sv.y);
+    x1 = fmaf(x1, sv.z, sv.w);
+    if constexpr (PELU) {
+      x0 = elu_max(x0);
+      x1 = elu_max(x1);
+    }
+    if constexpr (ZP) {
+      const bool ok = (uvalid >> k) & 1u;
+      x0 = ok ? x0 : 0.f;
+      x1 = ok ? x1 : 0.f;
+    }
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    bf16x2 hi;
+    hi[0] = (__bf16)x0;
+    hi[1] = (__bf16)x1;
+    char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 8 + h * 4;
+    *reinterpret_cast<bf16x2*>(dst) = hi;
+    if constexpr (MODE == MODE_F32X3) {
+      bf16x2 lo;
+      lo[0] = (__bf16)(x0 - (float)hi[0]);
+      lo[1] = (__bf16)(x1 - (float)hi[1]);
+      *reinterpret_cast<bf16x2*>(dst + 64) = lo;
+    }
+  };
+
+  SDP_T(1);
+  // ---- prologue: chunk 0 staged + transformed, chunk 1 in flight ----
+  load_b(std::integral_constant<int, 0>{}, 0, 0);
+  if constexpr (NBUF == 3) load_b(std::integral_constant<int, 1>{}, 0, 1);
+  load_ss(0);
+  static_for<0, NU>([&](auto k) { load_unit(k, 0); });
+  static_for<0, NU>([&](auto k) { xform_unit(k, std::integral_constant<int, 0>{}); });
+  if (nchunks > 1) {
+    load_ss(1);
+    static_for<0, NU>([&](auto k) { load_unit(k, 1); });
+  }
+  __syncthreads();
+  SDP_T(2);
+
+  // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel
+  auto read_a = [&](const char* pat, auto tap_c, auto s_c, bf16x8* hi, bf16x8* lo) __attribute__((always_inline)) {
+    constexpr int tap = decltype(tap_c)::value, s = decltype(s_c)::value;
+    constexpr int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
+    static_for<0, 4>([&](auto mbc) {
+      constexpr int mb = decltype(mbc)::value;
+      constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
+      const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off + s * 32;
+      hi[mb] = *reinterpret_cast<const bf16x8*>(src);
+      if constexpr (MODE == MODE_F32X3) lo[mb] = *reinterpret_cast<const bf16x8*>(src + 64);
+    });
+  };
+
+  auto do_chunk = [&](auto parity, int chunk) __attribute__((always_inline)) {
+    constexpr int P = decltype(parity)::value;
+    // The transform of chunk+1 and the DMA of chunk+2 run unconditionally (branch-free
+    // regions schedule across the MFMAs); past the last chunk they touch only dead buffers.
+    const char* pat = lds + P * T::PATCH_BYTES;
+    bf16x8 pre_hi[4], pre_lo[4];   // s=0 fragments of the next tap, read one region ahead
+    if constexpr (MODE != MODE_F32) read_a(pat, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                                           pre_hi, pre_lo);
+    static_for<0, NT>([&](auto tap_c) {
+      constexpr int tap = decltype(tap_c)::value;
+      constexpr int DIST = NBUF - 1;                       // prefetch distance in taps
+      constexpr int CUR = NBUF == 3 ? tap % 3 : (tap + P) & 1;
+      constexpr int NXT = NBUF == 3 ? (tap + DIST) % 3 : (tap + 1 + P) & 1;
+      if constexpr (tap + DIST < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + DIST);
+      else load_b(std::integral_constant<int, NXT>{}, min(chunk + 1, nchunks - 1), tap + DIST - NT);
+      __builtin_amdgcn_sched_barrier(0);
+      // next chunk's transform on taps [0, XT), then the chunk after next's DMA on the rest
+      // this tap's share of the next chunk's transform (units k with k % XT == tap)
+      constexpr int NX = (tap < XT) ? (NU - tap + XT - 1) / XT : 0;
+      float4 xv[NX > 0 ? NX : 1];
+      auto xform_loads = [&]() __attribute__((always_inline)) {
+        static_for<0, NX>([&](auto j) { xv[j] = xform_load(std::integral_constant<int, tap + XT * j>{}); });
+      };
+      auto xform_stores = [&]() __attribute__((always_inline)) {
+        static_for<0, NX>([&](auto j) {
+          xform_store(std::integral_constant<int, tap + XT * j>{}, std::integral_constant<int, 1 - P>{}, xv[j]);
+        });
+      };
+      auto dmas = [&]() __attribute__((always_inline)) {
+        if constexpr (tap == NT - 1) load_ss(min(chunk + 2, nchunks - 1));
+        static_for<0, NU>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          constexpr int dt = NT > XT ? XT : 0;   // all at the first free tap: the longest flight
+          if constexpr (dt == tap) load_unit(kc, chunk + 2);
+        });
+      };
+      if constexpr (MODE == MODE_F32) {
+        xform_loads();
+        xform_stores();
+        if constexpr (NT == 1) __builtin_amdgcn_sched_barrier(0);
+        dmas();
+        const int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {   // k steps [8*half, 8*half+8)
+          float av[4][8];
+          static_for<0, 4>([&](auto mbc) {
+            constexpr int mb = decltype(mbc)::value;
+            constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
+            const int pix = (wrow0 + mr + kh) * T::PC + mc + (lane & 31) + kw;
+            const char* src = pat + pix * PSTRIDE + (lane >> 5) * 64 + half * 32;
+            const float4 f0 = *reinterpret_cast<const float4*>(src);
+            const float4 f1 = *reinterpret_cast<const float4*>(src + 16);
+            av[mb][0] = f0.x; av[mb][1] = f0.y; av[mb][2] = f0.z; av[mb][3] = f0.w;
+            av[mb][4] = f1.x; av[mb][5] = f1.y; av[mb][6] = f1.z; av[mb][7] = f1.w;
+          });
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk) {
+            const int k = half * 8 + kk;
+            static_for<0, 2>([&](auto nbc) {
+              constexpr int nb = decltype(nbc)::value;
+              const uint4 bv = bq[CUR][nb][k >> 2];
+              const uint32_t bw = (k & 3) == 0 ? bv.x : (k & 3) == 1 ? bv.y : (k & 3) == 2 ? bv.z : bv.w;
+              const float bf = __uint_as_float(bw);
+              static_for<0, 4>([&](auto mbc) {
+                constexpr int mb = decltype(mbc)::value;
+                acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mb][kk], bf, acc[mb][nb], 0, 0, 0);
+              });
+            });
+          }
+        }
+      } else {
+        // Explicitly interleaved: 16 blocks of (s, nb, mb) -> 3 MFMAs (fp32x3) each, every
+        // block its own scheduling region carrying one piece (2 channels) of the next chunk's
+        // transform, so the VALU issues in the MFMA shadow.  Reads: this tap's raw units
+        // first (their lgkmcnt retires first), then A(tap, s=1), then A(tap+1, s=0).
+        float4 xv[NX > 0 ? NX : 1];
+        static_for<0, NX>([&](auto j) { xv[j] = xform_load(std::integral_constant<int, tap + XT * j>{}); });
+        bf16x8 c0_hi[4], c0_lo[4], c1_hi[4], c1_lo[4];
+        static_for<0, 4>([&](auto mb) {
+          c0_hi[mb] = pre_hi[mb];
+          if constexpr (MODE == MODE_F32X3) c0_lo[mb] = pre_lo[mb];
+        });
+        read_a(pat, tap_c, std::integral_constant<int, 1>{}, c1_hi, c1_lo);
+        if constexpr (tap + 1 < NT)
+          read_a(pat, std::integral_constant<int, tap + 1>{}, std::integral_constant<int, 0>{}, pre_hi, pre_lo);
+        if constexpr (NT > 1) dmas();   // 1x1: after the blocks, behind this tap's raw reads
+        static_for<0, 16>([&](auto blk_c) {
+          constexpr int blk = decltype(blk_c)::value;
+          constexpr int s = blk >> 3, nb = (blk >> 2) & 1, mb = blk & 3;
+          const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
+          const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
+          const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
+          const bf16x8 ahi = s == 0 ? c0_hi[mb] : c1_hi[mb];
+          if constexpr (MODE == MODE_F32X3) {
+            const bf16x8 alo = s == 0 ? c0_lo[mb] : c1_lo[mb];
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[mb][nb], 0, 0, 0);
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[mb][nb], 0, 0, 0);
+          }
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[mb][nb], 0, 0, 0);
+          if constexpr (blk < 2 * NX) xform_piece(std::integral_constant<int, tap + XT * (blk >> 1)>{},
+                                                  std::integral_constant<int, blk & 1>{},
+                                                  std::integral_constant<int, 1 - P>{}, xv[blk >> 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        if constexpr (NT == 1) dmas();
+      }
+    });
+    // patch[P] free for chunk+2's transform, patch[1-P] complete.  A raw barrier: only the
+    // LDS writes must have landed; the DMA of chunk+2 and the weight loads stay in flight.
+#ifdef SDP_TIMING
+    const unsigned long long tb0 = __builtin_amdgcn_s_memtime();
+#endif
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    if constexpr (!(SDP_KO & 8)) __builtin_amdgcn_s_barrier();
+#ifdef SDP_TIMING
+    tbar += __builtin_amdgcn_s_memtime() - tb0;
+#endif
+  };
+  static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
+  for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
+    do_chunk(std::integral_constant<int, 0>{}, chunk);
+    do_chunk(std::integral_constant<int, 1>{}, chunk + 1);
+  }
+
+  SDP_T(3);
+  // ------------------------------------------------------------------ epilogue
+  // The accumulators go through LDS (the patch/raw buffers are free now) in two halves of
+  // 64 pixels per wave, so the output is written as whole pixel rows -- every thread owns 4
+  // consecutive channels of a pixel, every store/load is 16 B and a wave instruction covers
+  // 1 KiB (Cout 256) or two 512-B rows -- with bias, 2x2 mean-pool, residual, bilinear
+  // upsample-add, the CRP second output, ELU and the InstanceNorm++ statistics applied on
+  // the way.
+  __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
+  __syncthreads();
+  constexpr int SROW = T::NTILE + 8;               // staged row stride (floats): conflict-free writes
+  constexpr int SP = WM * 64;                      // staged pixels per half
+  constexpr int CG = T::NTILE / 4;                 // 16-B channel groups per pixel
+  constexpr int PL = 256 / CG;                     // threads per channel group
+  constexpr int NPO = POOL ? SP / 4 : SP;          // output pixels per half
+  static_assert(SP * SROW * 4 <= T::LDS_BYTES, "epilogue staging fits the LDS");
+  float* stage = reinterpret_cast<float*>(lds);
+  const int cg = tid % CG, pl = tid / CG;
+  const int co0 = n0 + cg * 4;                     // this thread's 4 output channels
+  const float4 bias4 = a.bias ? ld4(a.bias + co0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
+  float* outb = a.out + (size_t)b * Ho * Wo * Cout;
+  // shifted sums per (stats group, channel): K = the thread's first value
+  float4 sK[WM], s1[WM], s2[WM];
+  int sn[WM];
+  static_for<0, WM>([&](auto g) {
+    sK[g] = make_float4(0.f, 0.f, 0.f, 0.f); s1[g] = sK[g]; s2[g] = sK[g]; sn[g] = 0;
+  });
+  static_for<0, 2>([&](auto hc) {
+    constexpr int h = decltype(hc)::value;
+    // ---- stage this half's accumulators: wave (wm, wn), fragments mb of the half
+    static_for<0, 2>([&](auto ic) {
+      constexpr int mb = POOL ? (h + 2 * decltype(ic)::value) : (2 * h + decltype(ic)::value);
+      constexpr int q0 = decltype(ic)::value * 32;
+      static_for<0, 2>([&](auto nbc) {
+        constexpr int nb = decltype(nbc)::value;
+        float* dst = stage + (wm * 64 + q0 + 4 * (lane >> 5)) * SROW + wn * 64 + nb * 32 + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * SROW] = acc[mb][nb][r];
+      });
+    });
+    __syncthreads();
+    // ---- row phase: output pixels j = pl, pl + PL, ... of this half
+#pragma unroll 2
+    for (int j = pl; j < NPO; j += PL) {
+      float4 v;
+      int y, x, g;
+      if constexpr (POOL) {
+        // staged pixel s = row*32 + col over rows 0/1 and columns [32h, 32h+32)
+        const float* s0 = stage + (2 * j) * SROW + cg * 4;
+        const float4 o00 = ld4(s0), o01 = ld4(s0 + SROW), o10 = ld4(s0 + 32 * SROW), o11 = ld4(s0 + 33 * SROW);
+        auto pool1 = [&](float a00, float a10, float a01, float a11, float bb) {
+          return ((((a00 + bb) + (a10 + bb)) + (a01 + bb)) + (a11 + bb)) / 4.0f;  // layers.py:310-312
+        };
+        v.x = pool1(o00.x, o10.x, o01.x, o11.x, bias4.x);
+        v.y = pool1(o00.y, o10.y, o01.y, o11.y, bias4.y);
+        v.z = pool1(o00.z, o10.z, o01.z, o11.z, bias4.z);
+        v.w = pool1(o00.w, o10.w, o01.w, o11.w, bias4.w);
+        y = (sr0 + wrow0) >> 1;
+        x = (sc0 + 32 * h + 2 * j) >> 1;
+        g = 0;
+      } else {
+        const float4 o = ld4(stage + j * SROW + cg * 4);
+        v = make_float4(o.x + bias4.x, o.y + bias4.y, o.z + bias4.z, o.w + bias4.w);
+        const int ws = j >> 6, q = j & 63;                 // staged pixel -> (wave row block, pixel)
+        const int mb = 2 * h + (q >> 5);
+        const int row = ws * T::RW + mb / (TC / 32), col = (mb % (TC / 32)) * 32 + (q & 31);
+        y = (sr0 + row) * d + ph_r;
+        x = (sc0 + col) * d + ph_c;
+        g = ws;
+      }
+      const size_t oidx = ((size_t)y * Wo + x) * Cout + co0;
+      if (a.up) {
+        // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor at (y, x)
+        const int Hi = a.H / 2, Wi = a.W / 2;
+        const float sh = (float)(Hi - 1) / (float)(a.H - 1), sw = (float)(Wi - 1) / (float)(a.W - 1);
+        const float fy = sh * (float)y, fx = sw * (float)x;
+        const int y0 = (int)fy, x0 = (int)fx;
+        const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
+        const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co0;
+        const float4 v00 = ld4(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = ld4(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
+        const float4 v10 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
+        const float4 v11 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
+        auto bil = [&](float a00, float a01, float a10, float a11) {
+          return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+        };
+        v.x = v.x + bil(v00.x, v01.x, v10.x, v11.x);
+        v.y = v.y + bil(v00.y, v01.y, v10.y, v11.y);
+        v.z = v.z + bil(v00.z, v01.z, v10.z, v11.z);
+        v.w = v.w + bil(v00.w, v01.w, v10.w, v11.w);
+      }
+      const size_t bo = (size_t)b * Ho * Wo * Cout;
+      if (a.dact) {
+        // backward: scale by the derivative of the ELU that followed this tensor in the forward
+        //   1: aux = pre-activation h          elu'(h) = h > 0 ? 1 : e^h
+        //   2: aux = post-activation ELU(h)    elu'    = y > 0 ? 1 : y + 1
+        //   3: aux = InstanceNorm++ input h, z = h*scale + shift (epi_ss)  elu'(z)
+        float4 h4 = ld4(a.aux + bo + oidx);
+        if (a.dact == 3) {
+          const float4 s0 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2), s1 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2 + 4);
+          h4 = make_float4(fmaf(h4.x, s0.x, s0.y), fmaf(h4.y, s0.z, s0.w), fmaf(h4.z, s1.x, s1.y), fmaf(h4.w, s1.z, s1.w));
+        }
+        v = make_float4(v.x * elu_grad(h4.x, a.dact), v.y * elu_grad(h4.y, a.dact), v.z * elu_grad(h4.z, a.dact),
+                        v.w * elu_grad(h4.w, a.dact));
+      }
+      if (a.res) {
+        const float4 r4 = ld4(a.res + bo + oidx);
+        v = make_float4(r4.x + v.x, r4.y + v.y, r4.z + v.z, r4.w + v.w);
+      }
+      if (a.out2) {
+        const float4 r4 = ld4(a.res2 + bo + oidx);
+        *reinterpret_cast<float4*>(a.out2 + bo + oidx) = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
+      }
+      if (a.epi_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
+      if constexpr (!(SDP_KO & 16)) *reinterpret_cast<float4*>(outb + oidx) = v;
+      static_for<0, WM>([&](auto gc) {
+        constexpr int gg = decltype(gc)::value;
+        if (gg == g) {
+          if (sn[gg] == 0) sK[gg] = v;
+          const float4 dv = make_float4(v.x - sK[gg].x, v.y - sK[gg].y, v.z - sK[gg].z, v.w - sK[gg].w);
+          s1[gg] = make_float4(s1[gg].x + dv.x, s1[gg].y + dv.y, s1[gg].z + dv.z, s1[gg].w + dv.w);
+          s2[gg] = make_float4(fmaf(dv.x, dv.x, s2[gg].x), fmaf(dv.y, dv.y, s2[gg].y), fmaf(dv.z, dv.z, s2[gg].z),
+                               fmaf(dv.w, dv.w, s2[gg].w));
+          ++sn[gg];
+        }
+      });
+    }
+    __syncthreads();   // staging buffer reused by the next half / the statistics
+  });
+
+  if (a.stats) {
+    // per-thread partials -> (mean, M2) in LDS, then a Chan merge over the PL threads of a
+    // channel group; one 128-pixel statistics group per wave row block (WM)
+    float2* part = reinterpret_cast<float2*>(lds);   // [WM][PL][NTILE]
+    static_for<0, WM>([&](auto gc) {
+      constexpr int gg = decltype(gc)::value;
+      const float n = (float)sn[gg], inv = sn[gg] ? 1.f / n : 0.f;
+      const float k4[4] = {sK[gg].x, sK[gg].y, sK[gg].z, sK[gg].w};
+      const float a4[4] = {s1[gg].x, s1[gg].y, s1[gg].z, s1[gg].w};
+      const float q4[4] = {s2[gg].x, s2[gg].y, s2[gg].z, s2[gg].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float mean = k4[c] + a4[c] * inv;
+        const float m2 = fmaxf(q4[c] - a4[c] * a4[c] * inv, 0.f);
+        part[(gg * PL + pl) * T::NTILE + cg * 4 + c] = make_float2(mean, m2);
+      }
+    });
+    __syncthreads();
+    constexpr int PER = (POOL ? 32 : 128) / PL;      // values per thread per statistics group
+    for (int i = tid; i < WM * T::NTILE; i += 256) {
+      const int gg = i / T::NTILE, co = i % T::NTILE;
+      float mean = 0.f;
+      for (int k = 0; k < PL; ++k) mean += part[(gg * PL + k) * T::NTILE + co].x;
+      mean *= 1.f / PL;
+      float m2 = 0.f;
+      for (int k = 0; k < PL; ++k) {
+        const float2 pk = part[(gg * PL + k) * T::NTILE + co];
+        const float dm = pk.x - mean;
+        m2 += pk.y + (float)PER * dm * dm;
+      }
+      float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile * WM + gg) * Cout + n0 + co;
+      *st = make_float2(mean, m2);
+    }
+  }
+#ifdef SDP_TIMING
+  SDP_T(4);
+  if (tid == 0) {
+    unsigned long long* o = a.dbg + blockIdx.x * 8;
+    o[0] = tclk[0]; o[1] = tclk[1]; o[2] = tclk[2]; o[3] = tclk[3]; o[4] = tclk[4]; o[5] = tbar;
+  }
+#endif
+#endif
+}
+
+}  // namespace sdp

@@ -10,12 +10,38 @@ hipError_t begin_conv(const float* x, const float* w, const float* bias, float* 
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st);
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
-                         const float* beta, float* ss, hipStream_t st);
+                         const float* beta, float* ss, hipStream_t st, float* nst = nullptr);
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st);
 hipError_t langevin_step(float* x, const float* g, const float* ref, const int32_t* mask, const float* noise,
                          uint64_t seed, uint64_t offset, float step, float nscale, float gref, int n2n, int B, int C,
                          int HW, float* lik_out, uint32_t* absmax, hipStream_t st);
 hipError_t axpy_step(float* x, const float* g, float a, const float* lik, const int32_t* mask, const float* ref, float b,
                      size_t n, hipStream_t st);
+
+// ---- training (DSM backward; train_aux.hip, wgrad.hip, conv_bwd.hip)
+hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k, int mode, int dgrad, hipStream_t st);
+hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
+                         int HW, int C, float* part, float* coef, float* dalpha, float* dgamma, float* dbeta,
+                         const float* r1, const float* r2, float* out, hipStream_t st);
+hipError_t chan_sum(const float* dy, size_t npix, int C, float* part, float* out, hipStream_t st);
+hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hipStream_t st);
+hipError_t maxpool5_backward(const float* src, const float* dp, const float* res, float* dst, uint8_t* idx, int B, int H,
+                             int W, int C, hipStream_t st);
+hipError_t upsample_backward(const float* g, float* dlow, int B, int H, int W, int C, int accumulate, hipStream_t st);
+hipError_t elu_backward_post(const float* dy, const float* y, const float* res, float* dst, size_t n, hipStream_t st);
+hipError_t add_tensors(const float* a, const float* b, float* dst, size_t n, hipStream_t st);
+hipError_t begin_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int H, int W,
+                            hipStream_t st);
+hipError_t end_conv_backward(const float* dscore, const float* sigmas, const int64_t* labels, const float* w,
+                             const float* o, const float* ss, float* g, float* part, float* dw, float* db, int B, int H,
+                             int W, hipStream_t st);
+hipError_t dsm_loss(const float* score, const float* noise, const float* mask, const float* used_sigma, int B, int n_img,
+                    float power, float* dscore, float* loss, float* loss_per, float* part, hipStream_t st);
+hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow, size_t n, float b1, float b2, float eps,
+                    float step_size, float bc2_sqrt, float mu, hipStream_t st);
+hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char** why);
+int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks);
+size_t wgrad_part_floats(int S, int Cin, int Cout, int ks);
+hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, int accumulate, hipStream_t st, const char** why);
 
 }  // namespace sdp

@@ -12,118 +12,12 @@
 #include <string>
 #include <vector>
 
-#include "../../include/sdp.h"
-#include "kernels.h"
 
-namespace sdp {
-
-struct HostParam {
-  std::vector<int64_t> shape;
-  std::vector<float> data;
-};
-
-static uint16_t f2bf(float f) {  // round-to-nearest-even (finite inputs)
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-static float bf2f(uint16_t h) {
-  uint32_t u = (uint32_t)h << 16;
-  float f;
-  std::memcpy(&f, &u, 4);
-  return f;
-}
-
-// Weight W[Cout][Cin][k][k] -> MFMA fragment order consumed by conv_mfma_kernel:
-//   [chunk = Cin/32][tap][nb = Cout/32][lane 64][16 x 4 bytes]
-// F32  : slot q of lane l = W[nb*32 + (l&31)][chunk*32 + 16*(l>>5) + q]
-// BF16 : slots = [s][hi 8 | lo 8] ; element j of lane l = ci chunk*32 + 16*s + 8*(l>>5) + j
-static std::vector<uint32_t> pack_conv_weights(const HostParam& p, int mode) {
-  const int Cout = (int)p.shape[0], Cin = (int)p.shape[1], k = (int)p.shape[2];
-  const int NT = k * k, NB = Cout / 32, NC = Cin / 32;
-  std::vector<uint32_t> out((size_t)Cout * Cin * NT);
-  for (int ch = 0; ch < NC; ++ch)
-    for (int tap = 0; tap < NT; ++tap)
-      for (int nb = 0; nb < NB; ++nb)
-        for (int lane = 0; lane < 64; ++lane) {
-          uint32_t* dst = &out[((((size_t)ch * NT + tap) * NB + nb) * 64 + lane) * 16];
-          const int co = nb * 32 + (lane & 31), h = lane >> 5;
-          auto wv = [&](int ci) { return p.data[((size_t)co * Cin + ci) * NT + tap]; };
-          if (mode == SDP_PREC_FP32) {
-            for (int q = 0; q < 16; ++q) {
-              const float f = wv(ch * 32 + 16 * h + q);
-              std::memcpy(&dst[q], &f, 4);
-            }
-          } else {
-            uint16_t* d16 = reinterpret_cast<uint16_t*>(dst);
-            for (int s = 0; s < 2; ++s)
-              for (int j = 0; j < 8; ++j) {
-                const float f = wv(ch * 32 + 16 * s + 8 * h + j);
-                const uint16_t hi = f2bf(f);
-                const uint16_t lo = f2bf(f - bf2f(hi));
-                d16[s * 16 + j] = hi;
-                d16[s * 16 + 8 + j] = lo;
-              }
-          }
-        }
-  return out;
-}
-
-}  // namespace sdp
+#include "net_internal.h"
 
 using namespace sdp;
 
-struct ProfRec {
-  std::string cls;
-  double flops;
-  hipEvent_t a, b;
-};
-
-struct sdp_net {
-  sdp_net_desc d;
-  bool profile = false;
-  std::vector<ProfRec> prof;        // events of the forwards since the last read
-  std::vector<hipEvent_t> ev_pool;
-  std::map<std::string, HostParam> host;
-  std::map<std::string, void*> dev;  // plain tensors and packed conv weights ("#frag" suffix)
-  bool finalized = false;
-  int mode = MODE_F32X3;
-
-  ~sdp_net() {
-    for (auto& kv : dev) (void)hipFree(kv.second);
-    for (auto& r : prof) {
-      (void)hipEventDestroy(r.a);
-      (void)hipEventDestroy(r.b);
-    }
-    for (auto e : ev_pool) (void)hipEventDestroy(e);
-  }
-  hipEvent_t event() {
-    if (!ev_pool.empty()) {
-      hipEvent_t e = ev_pool.back();
-      ev_pool.pop_back();
-      return e;
-    }
-    hipEvent_t e;
-    if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
-    return e;
-  }
-  const float* P(const std::string& k) const {
-    auto it = dev.find(k);
-    if (it == dev.end()) throw std::runtime_error("missing parameter " + k);
-    return reinterpret_cast<const float*>(it->second);
-  }
-  const float* Pn(const std::string& k) const {  // optional
-    auto it = dev.find(k);
-    return it == dev.end() ? nullptr : reinterpret_cast<const float*>(it->second);
-  }
-};
-
 namespace {
-
-void chk(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
-}
 
 struct Buf {
   float* p;
@@ -177,7 +71,7 @@ struct Fwd {
     if ((int)hp.shape[1] != in.C || (int)hp.shape[0] != out.C) throw std::runtime_error("conv shape mismatch " + wkey);
     const char* why = "conv launch";
     const int ks = (int)hp.shape[2];
-    ProfRec rec;
+    sdp_net::ProfRec rec;
     if (net->profile) {
       rec.cls = "conv" + std::to_string(ks) + "x" + std::to_string(ks) + " " + std::to_string(in.C) + "->" +
                 std::to_string(out.C) + " @" + std::to_string(in.H) + "x" + std::to_string(in.W) + " d" +
@@ -420,33 +314,97 @@ int sdp_net_set_param(sdp_net* net, const char* key, const float* data, const in
 int sdp_net_finalize(sdp_net* net) {
   if (!net) return fail("sdp_net_finalize: null net");
   try {
-    for (auto& kv : net->dev) chk(hipFree(kv.second), "hipFree");
-    net->dev.clear();
+    net->release();
+    if (!net->host.count("sigmas")) return fail("sdp_net_finalize: missing sigmas");
     auto upload = [&](const std::string& k, const void* src, size_t bytes) {
       void* d = nullptr;
       chk(hipMalloc(&d, bytes), "hipMalloc");
       chk(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice), "hipMemcpy");
       net->dev[k] = d;
     };
-    if (!net->host.count("sigmas")) return fail("sdp_net_finalize: missing sigmas");
+    // every learnable parameter in one arena, [key order][64-float aligned] (sdp_net_param_info)
+    net->layout.clear();
+    size_t off = 0;
     for (auto& kv : net->host) {
-      const std::string& k = kv.first;
+      if (kv.first == "sigmas") continue;
+      net->layout.push_back({kv.first, off, kv.second.data.size()});
+      off += (kv.second.data.size() + 63) / 64 * 64;
+    }
+    net->arena_floats = off;
+    chk(hipMalloc(&net->arena, off * 4), "hipMalloc");
+    net->arena_owned = true;
+    for (auto& e : net->layout) {
+      chk(hipMemcpy(net->arena + e.offset, net->host[e.key].data.data(), e.numel * 4, hipMemcpyHostToDevice), "hipMemcpy");
+      net->dev[e.key] = net->arena + e.offset;
+    }
+    upload("sigmas", net->host["sigmas"].data.data(), net->host["sigmas"].data.size() * 4);
+    for (auto& kv : net->host) {
       const HostParam& hp = kv.second;
-      upload(k, hp.data.data(), hp.data.size() * 4);
-      const bool is_conv_w = hp.shape.size() == 4 && k != "begin_conv.weight" && k != "end_conv.weight";
-      if (is_conv_w) {
-        if (hp.shape[0] % 32 || hp.shape[1] % 32) return fail("sdp_net_finalize: conv channels must be /32: " + k);
-        std::vector<uint32_t> fr = pack_conv_weights(hp, net->mode);
-        upload(k + "#frag", fr.data(), fr.size() * 4);
-      }
+      if (net->is_conv_w(kv.first) && (hp.shape[0] % 32 || hp.shape[1] % 32))
+        return fail("sdp_net_finalize: conv channels must be /32: " + kv.first);
     }
     // identity (scale, shift) = (1, 0) rows for convs without an InstanceNorm++ prologue
     std::vector<float> ident(2 * 1024);
     for (size_t i = 0; i < ident.size(); i += 2) ident[i] = 1.f;
     upload("#ident_ss", ident.data(), ident.size() * 4);
+    hipStream_t st;
+    chk(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    net->repack(st);
+    chk(hipStreamSynchronize(st), "hipStreamSynchronize");
+    chk(hipStreamDestroy(st), "hipStreamDestroy");
     net->finalized = true;
   } catch (const std::exception& e) {
     return fail(std::string("sdp_net_finalize: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_param_arena_floats(const sdp_net* net, size_t* n) {
+  if (!net || !n || !net->finalized) return fail("sdp_net_param_arena_floats: finalize first");
+  *n = net->arena_floats;
+  return 0;
+}
+
+int sdp_net_param_count(const sdp_net* net, int* n) {
+  if (!net || !n || !net->finalized) return fail("sdp_net_param_count: finalize first");
+  *n = (int)net->layout.size();
+  return 0;
+}
+
+int sdp_net_param_info(const sdp_net* net, int i, char* key, size_t cap, size_t* offset, size_t* numel) {
+  if (!net || !net->finalized || i < 0 || i >= (int)net->layout.size() || !key || cap == 0)
+    return fail("sdp_net_param_info: bad argument");
+  const auto& e = net->layout[i];
+  std::strncpy(key, e.key.c_str(), cap - 1);
+  key[cap - 1] = 0;
+  if (offset) *offset = e.offset;
+  if (numel) *numel = e.numel;
+  return 0;
+}
+
+int sdp_net_bind_params(sdp_net* net, float* arena, void* stream) {
+  if (!net || !arena || !net->finalized) return fail("sdp_net_bind_params: bad argument");
+  try {
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (arena != net->arena)
+      chk(hipMemcpyAsync(arena, net->arena, net->arena_floats * 4, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
+    chk(hipStreamSynchronize(st), "hipStreamSynchronize");
+    if (net->arena_owned) chk(hipFree(net->arena), "hipFree");
+    net->arena = arena;
+    net->arena_owned = false;
+    for (auto& e : net->layout) net->dev[e.key] = arena + e.offset;
+  } catch (const std::exception& e) {
+    return fail(std::string("sdp_net_bind_params: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_repack(sdp_net* net, void* stream) {
+  if (!net || !net->finalized) return fail("sdp_net_repack: finalize first");
+  try {
+    net->repack(reinterpret_cast<hipStream_t>(stream));
+  } catch (const std::exception& e) {
+    return fail(std::string("sdp_net_repack: ") + e.what());
   }
   return 0;
 }

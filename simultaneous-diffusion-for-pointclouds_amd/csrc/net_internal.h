@@ -1,0 +1,123 @@
+// sdp_net handle internals, shared by the forward runtime (net.hip) and the training
+// runtime (train.hip).
+#pragma once
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/sdp.h"
+#include "kernels.h"
+
+namespace sdp {
+
+struct HostParam {
+  std::vector<int64_t> shape;
+  std::vector<float> data;
+};
+
+struct ParamEntry {
+  std::string key;
+  size_t offset, numel;   // floats within the parameter arena
+};
+
+inline void chk(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct TrainPlan;   // train.hip
+void destroy_plan(TrainPlan* p);
+
+}  // namespace sdp
+
+struct sdp_net {
+  struct ProfRec {
+    std::string cls;
+    double flops;
+    hipEvent_t a, b;
+  };
+  sdp_net_desc d;
+  bool profile = false;
+  std::vector<ProfRec> prof;        // events of the forwards since the last read
+  std::vector<hipEvent_t> ev_pool;
+  std::map<std::string, sdp::HostParam> host;
+  // device tensors: parameters (pointers into `arena`), "sigmas", "#ident_ss" and the packed
+  // conv weights "<key>#frag" (forward) / "<key>#dfrag" (data gradient, training only)
+  std::map<std::string, void*> dev;
+  std::vector<sdp::ParamEntry> layout;
+  float* arena = nullptr;           // every learnable parameter, fp32, `layout` order
+  size_t arena_floats = 0;
+  bool arena_owned = false;         // false once the caller bound its own arena
+  bool finalized = false;
+  bool train_packs = false;         // keep the dgrad packings current in repack()
+  int mode = sdp::MODE_F32X3;
+  sdp::TrainPlan* plan = nullptr;   // tape of the last sdp_net_forward_train
+
+  ~sdp_net() {
+    release();
+    for (auto& r : prof) {
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+  }
+  void release() {
+    for (auto& kv : dev) {
+      const bool in_arena = arena && kv.second >= (void*)arena && kv.second < (void*)(arena + arena_floats);
+      if (!in_arena) (void)hipFree(kv.second);
+    }
+    dev.clear();
+    if (arena_owned && arena) (void)hipFree(arena);
+    arena = nullptr;
+    arena_owned = false;
+    if (plan) sdp::destroy_plan(plan);
+    plan = nullptr;
+  }
+  hipEvent_t event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
+    return e;
+  }
+  const float* P(const std::string& k) const {
+    auto it = dev.find(k);
+    if (it == dev.end()) throw std::runtime_error("missing parameter " + k);
+    return reinterpret_cast<const float*>(it->second);
+  }
+  float* grad_of(float* grads, const std::string& k) const {
+    for (auto& e : layout)
+      if (e.key == k) return grads + e.offset;
+    throw std::runtime_error("no parameter " + k);
+  }
+  bool is_conv_w(const std::string& k) const {
+    auto it = host.find(k);
+    return it != host.end() && it->second.shape.size() == 4 && k != "begin_conv.weight" && k != "end_conv.weight";
+  }
+  // (re)build the fragment-ordered weights from the fp32 parameters on the device
+  void repack(hipStream_t st) {
+    for (auto& kv : host) {
+      if (!is_conv_w(kv.first)) continue;
+      const auto& s = kv.second.shape;
+      const size_t bytes = kv.second.data.size() * 4;
+      for (int dg = 0; dg < (train_packs ? 2 : 1); ++dg) {
+        const std::string fk = kv.first + (dg ? "#dfrag" : "#frag");
+        if (!dev.count(fk)) {
+          void* d = nullptr;
+          sdp::chk(hipMalloc(&d, bytes), "hipMalloc");
+          dev[fk] = d;
+        }
+        sdp::chk(sdp::pack_weights(P(kv.first), reinterpret_cast<uint32_t*>(dev[fk]), (int)s[0], (int)s[1], (int)s[2],
+                                   mode, dg, st),
+                 "pack_weights");
+      }
+    }
+  }
+};
+
+int sdp_fail(const std::string& m);

@@ -1,0 +1,587 @@
+// DSM training runtime of NCSN_LiDAR_small (BASELINE config 5):
+//   sdp_net_forward_train : the score-net forward of ncsnv2.py:484-518 with every tensor the
+//                           backward needs kept in the caller's workspace (the "tape")
+//   sdp_net_backward      : d loss / d parameters for a given d loss / d score -- loss.backward()
+//                           of runners/ncsn_runner_kitti_simultaneous.py:229-232 -- written into a
+//                           caller-owned gradient arena laid out like the parameter arena
+//   sdp_dsm_loss          : anneal_dsm_score_estimation_with_mask (losses/dsm.py:67-119)
+//   sdp_adam_ema_step     : optimizer.step() of torch.optim.Adam + EMAHelper.update (ema.py:16-21)
+//
+// The forward mirrors net.hip's fused plan (InstanceNorm++ statistics in conv epilogues, its
+// affine + ELU in the consumer's prologue, residual / upsample / CRP sums as epilogues) but
+// keeps its tensors.  The backward walks the graph in reverse with
+//   data gradients  : conv_mfma_kernel on dy with flipped/transposed weights (conv_bwd.hip),
+//                     fusing elu' and residual gradients into its epilogue,
+//   weight gradients: conv_wgrad_kernel (wgrad.hip, MFMA with LDS transpose reads),
+//   the rest        : train_aux.hip (IN++ backward, pooling / upsampling adjoints, biases).
+// Workspace = forward tape + backward buffers, bump-allocated in a fixed order; a dry run of
+// the same code computes its size (sdp_net_train_workspace_size).
+#include <cmath>
+
+#include "net_internal.h"
+
+namespace sdp {
+
+struct T4 {
+  float* p;
+  int H, W, C;
+};
+
+struct TrainPlan {
+  sdp_net* net = nullptr;
+  int B = 0, H = 0, W = 0, C = 0;
+  hipStream_t st = nullptr;
+  bool dry = true;
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+  std::map<std::string, T4> saved;
+  std::map<std::string, float*> fl;   // saved per-norm tables: "<key>#ss", "<key>#nst"
+  float* stats = nullptr;
+  float* xin = nullptr;               // copy of the forward input [B,2,H,W]
+  int64_t* lab = nullptr;             // copy of the labels
+  // backward scratch
+  float *wpart = nullptr, *spart = nullptr, *coef = nullptr, *cpart = nullptr, *epart = nullptr;
+  uint8_t* idx = nullptr;
+  size_t wpart_n = 0;
+  float* grads = nullptr;
+  size_t fwd_bytes = 0;
+  size_t ws_need = 0;                 // forward + backward bytes (dry run), 0 = unknown
+
+  // ------------------------------------------------------------------ allocation
+  float* take(size_t nfloats) {
+    const size_t bytes = (nfloats * 4 + 255) / 256 * 256;
+    float* p = dry ? nullptr : reinterpret_cast<float*>(base + used);
+    used += bytes;
+    if (!dry && used > cap) throw std::runtime_error("training workspace too small");
+    return p;
+  }
+  T4 mk(int h, int w, int c) { return T4{take((size_t)B * h * w * c), h, w, c}; }
+  T4 like(const T4& t) { return mk(t.H, t.W, t.C); }
+  size_t n(const T4& t) const { return (size_t)B * t.H * t.W * t.C; }
+  void ok(hipError_t e, const std::string& what) {
+    if (e != hipSuccess) throw std::runtime_error(what + ": " + hipGetErrorString(e));
+  }
+  const float* P(const std::string& k) const { return net->P(k); }
+  float* G(const std::string& k) const { return dry ? nullptr : net->grad_of(grads, k); }
+  const T4& S(const std::string& k) const {
+    auto it = saved.find(k);
+    if (it == saved.end()) throw std::runtime_error("tape: missing " + k);
+    return it->second;
+  }
+  float* F(const std::string& k) const {
+    auto it = fl.find(k);
+    if (it == fl.end()) throw std::runtime_error("tape: missing " + k);
+    return it->second;
+  }
+  int ks_of(const std::string& wkey) const { return (int)net->host.at(wkey + ".weight").shape[2]; }
+
+  // ------------------------------------------------------------------ forward pieces
+  struct Opt {
+    int pro = PRO_NONE;
+    const float* ss = nullptr;
+    bool bias = true;
+    const float* res = nullptr;
+    const float* up = nullptr;
+    float* out2 = nullptr;
+    const float* res2 = nullptr;
+    bool epi_elu = false;
+    bool stats = false;
+    int dil = 1;
+    bool circular = true;
+    bool pool = false;
+  };
+  void conv(const T4& in, const std::string& wkey, const T4& out, const Opt& o) {
+    const auto& hp = net->host.at(wkey + ".weight");
+    if ((int)hp.shape[1] != in.C || (int)hp.shape[0] != out.C) throw std::runtime_error("conv shape mismatch " + wkey);
+    if (dry) return;
+    ConvArgs a{};
+    a.in = in.p;
+    a.wf = reinterpret_cast<const uint4*>(P(wkey + ".weight#frag"));
+    a.bias = o.bias ? P(wkey + ".bias") : nullptr;
+    a.out = out.p;
+    a.res = o.res;
+    a.out2 = o.out2;
+    a.res2 = o.res2;
+    a.up = o.up;
+    a.pro_ss = o.pro == PRO_AFFINE_ELU ? o.ss : P("#ident_ss");
+    a.ss_bstride = o.pro == PRO_AFFINE_ELU ? 2 * in.C : 0;
+    a.stats = o.stats ? stats : nullptr;
+    a.B = B;
+    a.H = in.H;
+    a.W = in.W;
+    a.Cin = in.C;
+    a.Cout = out.C;
+    a.dil = o.dil;
+    a.circular = o.circular ? 1 : 0;
+    a.pro_mode = o.pro;
+    a.epi_elu = o.epi_elu ? 1 : 0;
+    const char* why = "conv launch";
+    ok(conv_mfma(net->mode, a, (int)hp.shape[2], o.pool, st, &why), std::string(why) + " (" + wkey + ")");
+  }
+  // statistics of the last stats-writing conv -> (scale, shift) + backward statistics of `nkey`
+  void norm(const std::string& nkey, int T, float cnt, int c) {
+    float* ss = take((size_t)B * c * 2);
+    float* nst = take((size_t)B * c * 4);
+    fl[nkey + "#ss"] = ss;
+    fl[nkey + "#nst"] = nst;
+    if (dry) return;
+    ok(inpp_finalize(stats, B, T, cnt, c, P(nkey + ".alpha"), P(nkey + ".gamma"), P(nkey + ".beta"), ss, st, nst),
+       "inpp_finalize " + nkey);
+  }
+  static int tiles(const T4& t) { return t.H * t.W / 128; }
+
+  // ResidualBlock.forward (layers.py:443-456)
+  T4 resf(const std::string& k, const T4& x, bool down, int dil, int x_tiles, float x_cnt) {
+    saved[k + ".x"] = x;
+    norm(k + ".normalize1", x_tiles, x_cnt, x.C);
+    T4 h1 = like(x);
+    Opt o1;
+    o1.pro = PRO_AFFINE_ELU;
+    o1.ss = F(k + ".normalize1#ss");
+    o1.stats = true;
+    o1.dil = dil;
+    conv(x, k + ".conv1", h1, o1);
+    saved[k + ".h1"] = h1;
+    norm(k + ".normalize2", tiles(h1), 128.f, h1.C);
+    Opt o2;
+    o2.pro = PRO_AFFINE_ELU;
+    o2.ss = F(k + ".normalize2#ss");
+    o2.stats = true;
+    o2.dil = dil;
+    T4 out;
+    if (down && dil == 1) {   // ConvMeanPool conv2 + ConvMeanPool 1x1 shortcut (layers.py:417-420)
+      T4 s = mk(x.H / 2, x.W / 2, 2 * x.C);
+      Opt os;
+      os.circular = false;
+      os.pool = true;
+      conv(x, k + ".shortcut.conv", s, os);
+      out = like(s);
+      o2.circular = false;
+      o2.pool = true;
+      o2.res = s.p;
+      conv(h1, k + ".conv2.conv", out, o2);
+    } else if (down) {         // dilated: no resampling, dilated shortcut (layers.py:411-415)
+      T4 s = like(x);
+      Opt os;
+      os.dil = dil;
+      conv(x, k + ".shortcut", s, os);
+      out = like(x);
+      o2.res = s.p;
+      conv(h1, k + ".conv2", out, o2);
+    } else {
+      out = like(x);
+      o2.res = x.p;
+      conv(h1, k + ".conv2", out, o2);
+    }
+    return out;
+  }
+  // RCUBlock (layers.py:126-134)
+  T4 rcuf(const std::string& k, T4 x, int nb, bool final_elu, bool final_stats) {
+    for (int i = 0; i < nb; ++i) {
+      const std::string c1 = k + "." + std::to_string(i + 1) + "_1_conv", c2 = k + "." + std::to_string(i + 1) + "_2_conv";
+      saved[k + ".x" + std::to_string(i)] = x;
+      T4 t = like(x);
+      Opt a;
+      a.pro = PRO_ELU;
+      a.bias = false;
+      conv(x, c1, t, a);
+      saved[k + ".t" + std::to_string(i)] = t;
+      T4 y = like(x);
+      Opt b;
+      b.pro = PRO_ELU;
+      b.bias = false;
+      b.res = x.p;
+      b.epi_elu = final_elu && i == nb - 1;
+      b.stats = final_stats && i == nb - 1;
+      conv(t, c2, y, b);
+      x = y;
+    }
+    saved[k + ".out"] = x;
+    return x;
+  }
+  // CRPBlock (layers.py:76-83) on X = ELU(h)
+  T4 crpf(const std::string& k, const T4& X) {
+    saved[k + ".X"] = X;
+    T4 p1 = like(X), path1 = like(X), x1 = like(X), p2 = like(X), x2 = like(X);
+    if (!dry) ok(maxpool5(X.p, p1.p, B, X.H, X.W, X.C, st), "maxpool5");
+    Opt a;
+    a.bias = false;
+    a.out2 = x1.p;
+    a.res2 = X.p;
+    conv(p1, k + ".convs.0", path1, a);
+    if (!dry) ok(maxpool5(path1.p, p2.p, B, X.H, X.W, X.C, st), "maxpool5");
+    Opt b;
+    b.bias = false;
+    b.res = x1.p;
+    conv(p2, k + ".convs.1", x2, b);
+    saved[k + ".p1"] = p1;
+    saved[k + ".path1"] = path1;
+    saved[k + ".p2"] = p2;
+    return x2;
+  }
+  // RefineBlock (layers.py:234-249); MSF (layers.py:179-184) fused with the CRP's input ELU
+  T4 refinef(const std::string& k, const T4& a, const T4* b, int cout, int n_out, bool final_stats) {
+    T4 X;
+    if (!b) {
+      X = rcuf(k + ".adapt_convs.0", a, 2, true, false);
+    } else {
+      T4 hA = rcuf(k + ".adapt_convs.0", a, 2, false, false);
+      T4 hB = rcuf(k + ".adapt_convs.1", *b, 2, false, false);
+      if (hA.H == hB.H) {
+        T4 m0 = mk(hA.H, hA.W, cout);
+        conv(hA, k + ".msf.convs.0", m0, Opt{});
+        X = like(m0);
+        Opt o;
+        o.res = m0.p;
+        o.epi_elu = true;
+        conv(hB, k + ".msf.convs.1", X, o);
+      } else {
+        T4 m1 = mk(hB.H, hB.W, cout);
+        conv(hB, k + ".msf.convs.1", m1, Opt{});
+        X = mk(hA.H, hA.W, cout);
+        Opt o;
+        o.up = m1.p;
+        o.epi_elu = true;
+        conv(hA, k + ".msf.convs.0", X, o);
+      }
+      saved[k + ".msf.X"] = X;
+    }
+    T4 x2 = crpf(k + ".crp", X);
+    return rcuf(k + ".output_convs", x2, n_out, false, final_stats);
+  }
+
+  void forward(const float* x, const int64_t* labels, float* out) {
+    used = 0;
+    saved.clear();
+    fl.clear();
+    xin = take((size_t)B * 2 * H * W);
+    lab = reinterpret_cast<int64_t*>(take((size_t)B * 2));
+    if (!dry) {
+      ok(hipMemcpyAsync(xin, x, (size_t)B * 2 * H * W * 4, hipMemcpyDeviceToDevice, st), "copy x");
+      ok(hipMemcpyAsync(lab, labels, (size_t)B * 8, hipMemcpyDeviceToDevice, st), "copy labels");
+    }
+    stats = take((size_t)B * (H * W / 64) * 2 * C * 2);
+    T4 x0 = mk(H, W, C);
+    if (!dry)
+      ok(begin_conv(xin, P("begin_conv.weight"), P("begin_conv.bias"), x0.p, stats, B, H, W, st), "begin_conv");
+    T4 l1 = resf("res1.0", x0, false, 1, H * W / 64, 64.f);
+    l1 = resf("res1.1", l1, false, 1, tiles(l1), 128.f);
+    T4 l2 = resf("res2.0", l1, true, 1, tiles(l1), 128.f);
+    l2 = resf("res2.1", l2, false, 1, tiles(l1), 32.f);
+    T4 l3 = resf("res3.0", l2, true, 2, tiles(l2), 128.f);
+    l3 = resf("res3.1", l3, false, 2, tiles(l3), 128.f);
+    T4 l4 = resf("res4.0", l3, true, 4, tiles(l3), 128.f);
+    l4 = resf("res4.1", l4, false, 4, tiles(l4), 128.f);
+    T4 r1 = refinef("refine1", l4, nullptr, 2 * C, 1, false);
+    T4 r2 = refinef("refine2", l3, &r1, 2 * C, 1, false);
+    T4 r3 = refinef("refine3", l2, &r2, C, 1, false);
+    T4 o = refinef("refine4", l1, &r3, C, 3, true);
+    norm("normalizer", tiles(o), 128.f, C);
+    if (!dry)
+      ok(end_conv(o.p, F("normalizer#ss"), P("end_conv.weight"), P("end_conv.bias"), P("sigmas"), lab, out, B, H, W, C,
+                  st),
+         "end_conv");
+    fwd_bytes = used;
+  }
+
+  // ------------------------------------------------------------------ backward pieces
+  void wgrad(const std::string& k, const T4& in, int pro, const float* ss, const T4& dy, int dil, bool circular, int ks) {
+    if (dry) return;
+    WgradArgs a{};
+    a.in = in.p;
+    a.pro_ss = pro == PRO_AFFINE_ELU ? ss : P("#ident_ss");
+    a.ss_bstride = pro == PRO_AFFINE_ELU ? 2 * in.C : 0;
+    a.pro_mode = pro;
+    a.dy = dy.p;
+    a.part = wpart;
+    a.part_floats = wpart_n;
+    a.B = B;
+    a.H = in.H;
+    a.W = in.W;
+    a.Cin = in.C;
+    a.Cout = dy.C;
+    a.dil = dil;
+    a.circular = circular ? 1 : 0;
+    const char* why = "wgrad launch";
+    ok(conv_wgrad(net->mode, a, ks, G(k + ".weight"), 0, st, &why), std::string(why) + " (" + k + ")");
+  }
+  void dgrad(const std::string& k, const T4& dy, const T4& dx, int dil, bool circular, int ks, int dact,
+             const float* aux, const float* epi_ss, const float* res) {
+    if (dry) return;
+    ConvArgs a{};
+    a.in = dy.p;
+    a.wf = reinterpret_cast<const uint4*>(P(k + ".weight#dfrag"));
+    a.out = dx.p;
+    a.res = res;
+    a.pro_ss = P("#ident_ss");
+    a.B = B;
+    a.H = dy.H;
+    a.W = dy.W;
+    a.Cin = dy.C;
+    a.Cout = dx.C;
+    a.dil = dil;
+    a.circular = circular ? 1 : 0;
+    a.pro_mode = PRO_NONE;
+    a.aux = aux;
+    a.epi_ss = epi_ss;
+    a.dact = dact;
+    const char* why = "dgrad launch";
+    ok(conv_dgrad(net->mode, a, ks, st, &why), std::string(why) + " (" + k + ")");
+  }
+  void bias(const std::string& k, const T4& dy) {
+    if (dry) return;
+    ok(chan_sum(dy.p, (size_t)B * dy.H * dy.W, dy.C, cpart, G(k + ".bias"), st), "chan_sum " + k);
+  }
+  void inpp_back(const std::string& nkey, const T4& g, const T4& h, const float* r1, const float* r2, const T4& out) {
+    if (dry) return;
+    ok(inpp_backward(g.p, h.p, F(nkey + "#nst"), P(nkey + ".alpha"), P(nkey + ".gamma"), B, h.H * h.W, h.C, spart, coef,
+                     G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st),
+       "inpp_backward " + nkey);
+  }
+
+  T4 resb(const std::string& k, const T4& dout, bool down, int dil, const float* extra) {
+    const T4 &x = S(k + ".x"), &h1 = S(k + ".h1");
+    float *ss1 = F(k + ".normalize1#ss"), *ss2 = F(k + ".normalize2#ss");
+    T4 g2 = like(h1);
+    const float* sg;
+    if (down && dil == 1) {
+      T4 dyf = mk(x.H, x.W, dout.C);
+      if (!dry) ok(unpool(dout.p, dyf.p, B, x.H, x.W, dout.C, st), "unpool");
+      wgrad(k + ".conv2.conv", h1, PRO_AFFINE_ELU, ss2, dyf, 1, false, 3);
+      bias(k + ".conv2.conv", dyf);
+      dgrad(k + ".conv2.conv", dyf, g2, 1, false, 3, 3, h1.p, ss2, nullptr);
+      wgrad(k + ".shortcut.conv", x, PRO_NONE, nullptr, dyf, 1, false, 1);
+      bias(k + ".shortcut.conv", dyf);
+      T4 sgb = like(x);
+      dgrad(k + ".shortcut.conv", dyf, sgb, 1, false, 1, 0, nullptr, nullptr, nullptr);
+      sg = sgb.p;
+    } else {
+      wgrad(k + ".conv2", h1, PRO_AFFINE_ELU, ss2, dout, dil, true, 3);
+      bias(k + ".conv2", dout);
+      dgrad(k + ".conv2", dout, g2, dil, true, 3, 3, h1.p, ss2, nullptr);
+      if (down) {
+        wgrad(k + ".shortcut", x, PRO_NONE, nullptr, dout, dil, true, 3);
+        bias(k + ".shortcut", dout);
+        T4 sgb = like(x);
+        dgrad(k + ".shortcut", dout, sgb, dil, true, 3, 0, nullptr, nullptr, nullptr);
+        sg = sgb.p;
+      } else {
+        sg = dout.p;
+      }
+    }
+    T4 dh1 = like(h1);
+    inpp_back(k + ".normalize2", g2, h1, nullptr, nullptr, dh1);
+    wgrad(k + ".conv1", x, PRO_AFFINE_ELU, ss1, dh1, dil, true, 3);
+    bias(k + ".conv1", dh1);
+    T4 g1 = like(x);
+    dgrad(k + ".conv1", dh1, g1, dil, true, 3, 3, x.p, ss1, nullptr);
+    T4 dx = like(x);
+    inpp_back(k + ".normalize1", g1, x, sg, extra, dx);
+    return dx;
+  }
+  T4 rcub(const std::string& k, const T4& dxn, int nb, bool final_elu) {
+    T4 d = dxn;
+    if (final_elu) {
+      T4 d2 = like(dxn);
+      if (!dry) ok(elu_backward_post(dxn.p, S(k + ".out").p, nullptr, d2.p, n(d2), st), "elu_backward");
+      d = d2;
+    }
+    for (int i = nb - 1; i >= 0; --i) {
+      const std::string c1 = k + "." + std::to_string(i + 1) + "_1_conv", c2 = k + "." + std::to_string(i + 1) + "_2_conv";
+      const T4 &xi = S(k + ".x" + std::to_string(i)), &ti = S(k + ".t" + std::to_string(i));
+      wgrad(c2, ti, PRO_ELU, nullptr, d, 1, true, 3);
+      T4 dt = like(ti);
+      dgrad(c2, d, dt, 1, true, 3, 1, ti.p, nullptr, nullptr);
+      wgrad(c1, xi, PRO_ELU, nullptr, dt, 1, true, 3);
+      T4 dn = like(xi);
+      dgrad(c1, dt, dn, 1, true, 3, 1, xi.p, nullptr, d.p);
+      d = dn;
+    }
+    return d;
+  }
+  T4 crpb(const std::string& k, const T4& dx2) {
+    const T4 &X = S(k + ".X"), &p1 = S(k + ".p1"), &path1 = S(k + ".path1"), &p2 = S(k + ".p2");
+    wgrad(k + ".convs.1", p2, PRO_NONE, nullptr, dx2, 1, true, 3);
+    T4 dp2 = like(X);
+    dgrad(k + ".convs.1", dx2, dp2, 1, true, 3, 0, nullptr, nullptr, nullptr);
+    T4 dpath1 = like(X);
+    if (!dry) ok(maxpool5_backward(path1.p, dp2.p, dx2.p, dpath1.p, idx, B, X.H, X.W, X.C, st), "maxpool5_backward");
+    wgrad(k + ".convs.0", p1, PRO_NONE, nullptr, dpath1, 1, true, 3);
+    T4 dp1 = like(X);
+    dgrad(k + ".convs.0", dpath1, dp1, 1, true, 3, 0, nullptr, nullptr, nullptr);
+    T4 dX = like(X);
+    if (!dry) ok(maxpool5_backward(X.p, dp1.p, dx2.p, dX.p, idx, B, X.H, X.W, X.C, st), "maxpool5_backward");
+    return dX;
+  }
+  // returns the gradients of the refine block's inputs (second one empty for refine1)
+  std::pair<T4, T4> refineb(const std::string& k, const T4& dout, bool two, int n_out) {
+    T4 dx2 = rcub(k + ".output_convs", dout, n_out, false);
+    T4 dX = crpb(k + ".crp", dx2);
+    if (!two) return {rcub(k + ".adapt_convs.0", dX, 2, true), T4{}};
+    const T4 &X = S(k + ".msf.X"), &hA = S(k + ".adapt_convs.0.out"), &hB = S(k + ".adapt_convs.1.out");
+    T4 dm = like(X);
+    if (!dry) ok(elu_backward_post(dX.p, X.p, nullptr, dm.p, n(dm), st), "elu_backward");
+    T4 dm1 = dm;
+    if (hB.H != hA.H) {
+      dm1 = mk(hB.H, hB.W, X.C);
+      if (!dry) ok(upsample_backward(dm.p, dm1.p, B, X.H, X.W, X.C, 0, st), "upsample_backward");
+    }
+    wgrad(k + ".msf.convs.0", hA, PRO_NONE, nullptr, dm, 1, true, 3);
+    bias(k + ".msf.convs.0", dm);
+    T4 dhA = like(hA);
+    dgrad(k + ".msf.convs.0", dm, dhA, 1, true, 3, 0, nullptr, nullptr, nullptr);
+    wgrad(k + ".msf.convs.1", hB, PRO_NONE, nullptr, dm1, 1, true, 3);
+    bias(k + ".msf.convs.1", dm1);
+    T4 dhB = like(hB);
+    dgrad(k + ".msf.convs.1", dm1, dhB, 1, true, 3, 0, nullptr, nullptr, nullptr);
+    return {rcub(k + ".adapt_convs.0", dhA, 2, false), rcub(k + ".adapt_convs.1", dhB, 2, false)};
+  }
+
+  void backward(const float* dscore, float* grad_arena) {
+    used = fwd_bytes;
+    grads = grad_arena;
+    // scratch (upper bounds over every layer of the network)
+    wpart_n = (size_t)(512 + 64) * 9 * 128 * 32;
+    wpart = take(wpart_n);
+    spart = take((size_t)B * (H * W / 512) * 256 * 2);
+    coef = take((size_t)B * 256 * 4);
+    cpart = take(256 * 256);
+    epart = take(std::max((size_t)B * (H / 8) * (W / 32) * (2 * 128 * 9 + 2), (size_t)B * (H / 8) * (W / 64) * 128 * 37));
+    idx = reinterpret_cast<uint8_t*>(take((size_t)B * H * W * C / 4));
+    if (!dry) ok(hipMemsetAsync(grads, 0, net->arena_floats * 4, st), "zero grads");
+
+    // head: IN++ -> ELU -> end_conv -> / sigma
+    const T4& o = S("refine4.output_convs.out");
+    T4 g = like(o);
+    if (!dry)
+      ok(end_conv_backward(dscore, P("sigmas"), lab, P("end_conv.weight"), o.p, F("normalizer#ss"), g.p, epart,
+                           G("end_conv.weight"), G("end_conv.bias"), B, H, W, st),
+         "end_conv_backward");
+    T4 d_o = like(o);
+    inpp_back("normalizer", g, o, nullptr, nullptr, d_o);
+    auto r4 = refineb("refine4", d_o, true, 3);      // -> d L1 (part), d ref3
+    auto r3 = refineb("refine3", r4.second, true, 1);  // -> d L2 (part), d ref2
+    auto r2 = refineb("refine2", r3.second, true, 1);  // -> d L3 (part), d ref1
+    auto r1 = refineb("refine1", r2.second, false, 1); // -> d L4
+    T4 d = resb("res4.1", r1.first, false, 4, nullptr);
+    d = resb("res4.0", d, true, 4, r2.first.p);        // + d L3 from refine2
+    d = resb("res3.1", d, false, 2, nullptr);
+    d = resb("res3.0", d, true, 2, r3.first.p);        // + d L2 from refine3
+    d = resb("res2.1", d, false, 1, nullptr);
+    d = resb("res2.0", d, true, 1, r4.first.p);        // + d L1 from refine4
+    d = resb("res1.1", d, false, 1, nullptr);
+    d = resb("res1.0", d, false, 1, nullptr);
+    if (!dry)
+      ok(begin_conv_wgrad(xin, d.p, epart, G("begin_conv.weight"), G("begin_conv.bias"), B, H, W, st),
+         "begin_conv_wgrad");
+  }
+};
+
+void destroy_plan(TrainPlan* p) { delete p; }
+
+static TrainPlan* plan_for(sdp_net* net, int B) {
+  if (net->plan && net->plan->B == B) return net->plan;
+  if (net->plan) destroy_plan(net->plan);
+  TrainPlan* p = new TrainPlan();
+  p->net = net;
+  p->B = B;
+  p->H = net->d.H;
+  p->W = net->d.W;
+  p->C = net->d.ngf;
+  net->plan = p;
+  return p;
+}
+
+static size_t train_ws_bytes(sdp_net* net, int B) {
+  TrainPlan* p = plan_for(net, B);
+  if (p->ws_need) return p->ws_need;
+  p->dry = true;
+  p->forward(nullptr, nullptr, nullptr);
+  p->backward(nullptr, nullptr);
+  p->ws_need = p->used;
+  p->saved.clear();
+  p->fl.clear();
+  return p->ws_need;
+}
+
+}  // namespace sdp
+
+using namespace sdp;
+
+static int tfail(const std::string& m) { return sdp_fail(m); }
+
+static void enable_training(sdp_net* net, hipStream_t st) {
+  if (net->mode != MODE_F32X3 && net->mode != MODE_BF16) throw std::runtime_error("training needs fp32x3 or bf16");
+  if (!net->train_packs) {
+    net->train_packs = true;
+    net->repack(st);
+  }
+}
+
+extern "C" {
+
+int sdp_net_train_workspace_size(sdp_net* net, int B, size_t* bytes) {
+  if (!net || !bytes || B <= 0 || !net->finalized) return tfail("sdp_net_train_workspace_size: bad argument");
+  try {
+    *bytes = train_ws_bytes(net, B);
+  } catch (const std::exception& e) {
+    return tfail(std::string("sdp_net_train_workspace_size: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_forward_train(sdp_net* net, const float* x, const int64_t* labels, float* out, int B, void* ws,
+                          size_t ws_bytes, void* stream) {
+  if (!net || !x || !labels || !out || !ws || B <= 0) return tfail("sdp_net_forward_train: bad argument");
+  if (!net->finalized) return tfail("sdp_net_forward_train: call sdp_net_finalize first");
+  try {
+    const size_t need = train_ws_bytes(net, B);
+    if (ws_bytes < need) return tfail("sdp_net_forward_train: workspace too small");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    enable_training(net, st);
+    TrainPlan* p = plan_for(net, B);
+    p->dry = false;
+    p->st = st;
+    p->base = reinterpret_cast<char*>(ws);
+    p->cap = ws_bytes;
+    p->forward(x, labels, out);
+  } catch (const std::exception& e) {
+    return tfail(std::string("sdp_net_forward_train: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_backward(sdp_net* net, const float* dscore, int B, void* ws, size_t ws_bytes, float* grads, void* stream) {
+  if (!net || !dscore || !ws || !grads || B <= 0) return tfail("sdp_net_backward: bad argument");
+  TrainPlan* p = net->plan;
+  if (!p || p->dry || p->B != B || p->base != ws || p->saved.empty())
+    return tfail("sdp_net_backward: no tape -- call sdp_net_forward_train with this workspace and batch first");
+  try {
+    p->st = reinterpret_cast<hipStream_t>(stream);
+    p->cap = ws_bytes;
+    p->backward(dscore, grads);
+  } catch (const std::exception& e) {
+    return tfail(std::string("sdp_net_backward: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_dsm_loss(const float* score, const float* noise, const float* mask, const float* used_sigma, int B, int n_img,
+                 float anneal_power, float* dscore, float* loss, float* loss_per, float* part, void* stream) {
+  if (!score || !noise || !mask || !used_sigma || !dscore || !loss || !part || B <= 0 || n_img <= 0)
+    return tfail("sdp_dsm_loss: bad argument");
+  hipError_t e = dsm_loss(score, noise, mask, used_sigma, B, n_img, anneal_power, dscore, loss, loss_per, part,
+                          reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? 0 : tfail(std::string("sdp_dsm_loss: ") + hipGetErrorString(e));
+}
+
+int sdp_adam_ema_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema_shadow, size_t n,
+                      float lr, float beta1, float beta2, float eps, int step, float ema_mu, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || n == 0 || step < 1) return tfail("sdp_adam_ema_step: bad argument");
+  const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
+  hipError_t e = adam_ema(params, grads, exp_avg, exp_avg_sq, ema_shadow, n, beta1, beta2, eps, (float)(lr / bc1),
+                          (float)std::sqrt(bc2), ema_mu, reinterpret_cast<hipStream_t>(stream));
+  return e == hipSuccess ? 0 : tfail(std::string("sdp_adam_ema_step: ") + hipGetErrorString(e));
+}
+
+}  // extern "C"

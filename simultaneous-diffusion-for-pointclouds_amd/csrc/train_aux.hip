@@ -1,0 +1,728 @@
+// Memory-bound / small kernels of the DSM training step (BASELINE config 5):
+//   pack_weights   : fp32 [Cout][Cin][k][k] -> MFMA fragment order (forward, or the flipped +
+//                    transposed "dgrad" packing) on the device, so weights updated by the
+//                    optimizer are re-packed without a host round trip
+//   InstanceNorm++ backward (normalization.py:163-176): per-tile (sum g, sum g*xhat) ->
+//                    per-(b,c) coefficients dh = k1*g + k2*h + k3 and the alpha/gamma/beta
+//                    gradients -> the apply pass
+//   unpool         : adjoint of ConvMeanPool's 2x2 mean (layers.py:309-313)
+//   maxpool5 bwd   : adjoint of MaxPool2d(5, 1, 2) (layers.py:70), first-max tie rule
+//   upsample bwd   : adjoint of F.interpolate(bilinear, align_corners=True) (layers.py:182)
+//   elu bwd        : dy * elu'(from the ELU output)
+//   chan_sum       : bias gradients
+//   begin/end conv : weight gradients of the 4->128 / 128->2 convs, data gradient of end_conv
+//   dsm loss       : anneal_dsm_score_estimation_with_mask (losses/dsm.py:67-119) + d loss/d score
+//   adam_ema       : torch.optim.Adam step (losses/__init__.py:10-20) + EMAHelper.update (ema.py:16-21)
+#include "common.h"
+#include "kernels.h"
+
+namespace sdp {
+
+SDP_DEV float wsum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ---------------------------------------------------------------- weight packing
+// Fragment order consumed by conv_mfma_kernel: [chunk = Cin'/32][tap][nb = Cout'/32][lane 64][16 slots of 4 B]
+// F32  : slot q of lane l = W'[nb*32 + (l&31)][chunk*32 + 16*(l>>5) + q]
+// BF16 : 16-bit element (s, hl, j) of lane l, s in {0,1}, hl in {hi, lo}, j < 8:
+//        ci' = chunk*32 + 16*s + 8*(l>>5) + j ; hi = bf16(w), lo = bf16(w - hi)
+// dgrad: W'[o][i][tap] = W[i][o][k*k-1-tap]   (Cout' = Cin, Cin' = Cout)
+__global__ void pack_weights_kernel(const float* __restrict__ w, uint32_t* __restrict__ out, int Cout, int Cin, int NT,
+                                    int mode, int dgrad) {
+  const int Co = dgrad ? Cin : Cout, Ci = dgrad ? Cout : Cin;
+  const int NB = Co / 32;
+  const size_t n = (size_t)Co * Ci * NT;    // output 32-bit slots
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int slot = i & 15;
+    size_t r = i >> 4;
+    const int lane = r & 63;
+    r >>= 6;
+    const int nb = r % NB;
+    r /= NB;
+    const int tap = r % NT;
+    const int ch = r / NT;
+    const int co = nb * 32 + (lane & 31), h = lane >> 5;
+    auto wv = [&](int ci) -> float {
+      return dgrad ? w[((size_t)ci * Cin + co) * NT + (NT - 1 - tap)] : w[((size_t)co * Cin + ci) * NT + tap];
+    };
+    uint32_t v;
+    if (mode == MODE_F32) {
+      v = __float_as_uint(wv(ch * 32 + 16 * h + slot));
+    } else {
+      const int s = slot >> 3, hl = (slot >> 2) & 1, j0 = (slot & 3) * 2;
+      uint32_t pk = 0;
+      for (int e = 0; e < 2; ++e) {
+        const float f = wv(ch * 32 + 16 * s + 8 * h + j0 + e);
+        const __bf16 hi = (__bf16)f;
+        const __bf16 q = hl ? (__bf16)(f - (float)hi) : hi;
+        pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
+      }
+      v = pk;
+    }
+    out[i] = v;
+  }
+}
+
+hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k, int mode, int dgrad, hipStream_t st) {
+  const size_t n = (size_t)Cout * Cin * k * k;
+  const int grid = (int)std::min<size_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(grid), dim3(256), 0, st, w, out, Cout, Cin, k * k, mode, dgrad);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- InstanceNorm++ backward
+// part[b][grp][c] = (sum g, sum g * (h - mean) * rstd) over the 512 pixels of group grp
+__global__ __launch_bounds__(256) void inpp_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ h,
+                                                              const float4* __restrict__ nst, float2* __restrict__ part,
+                                                              int HW, int C) {
+  __shared__ float2 red[256 * 4];
+  const int b = blockIdx.y, grp = blockIdx.x, ngrp = gridDim.x;
+  const int C4 = C / 4, PL = 256 / C4, tid = threadIdx.x;
+  const int c4 = tid % C4, pl = tid / C4;
+  const size_t base = ((size_t)b * HW + (size_t)grp * 512) * C;
+  float4 mu, rs;
+  {
+    const float4 n0 = nst[(size_t)b * C + c4 * 4], n1 = nst[(size_t)b * C + c4 * 4 + 1];
+    const float4 n2 = nst[(size_t)b * C + c4 * 4 + 2], n3 = nst[(size_t)b * C + c4 * 4 + 3];
+    mu = make_float4(n0.x, n1.x, n2.x, n3.x);
+    rs = make_float4(n0.y, n1.y, n2.y, n3.y);
+  }
+  float sg[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int p = pl; p < 512; p += PL) {
+    const float4 gv = *reinterpret_cast<const float4*>(g + base + (size_t)p * C + c4 * 4);
+    const float4 hv = *reinterpret_cast<const float4*>(h + base + (size_t)p * C + c4 * 4);
+    sg[0] += gv.x; sg[1] += gv.y; sg[2] += gv.z; sg[3] += gv.w;
+    sx[0] = fmaf(gv.x, (hv.x - mu.x) * rs.x, sx[0]);
+    sx[1] = fmaf(gv.y, (hv.y - mu.y) * rs.y, sx[1]);
+    sx[2] = fmaf(gv.z, (hv.z - mu.z) * rs.z, sx[2]);
+    sx[3] = fmaf(gv.w, (hv.w - mu.w) * rs.w, sx[3]);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[(pl * C4 + c4) * 4 + k] = make_float2(sg[k], sx[k]);
+  __syncthreads();
+  for (int i = tid; i < C; i += 256) {
+    float a0 = 0.f, a1 = 0.f;
+    for (int k = 0; k < PL; ++k) {
+      const float2 v = red[(k * C4 + i / 4) * 4 + (i & 3)];
+      a0 += v.x;
+      a1 += v.y;
+    }
+    part[((size_t)b * ngrp + grp) * C + i] = make_float2(a0, a1);
+  }
+}
+
+// One 1024-thread block.  Per image: G_c, Gx_c (f64 over the groups), then the channel-mean
+// path of IN++: mhat = (mu - m)/sqrt(v + eps) with the unbiased v over C channels.
+//   dh = gamma*rstd*(g - G/N - xhat*Gx/N) + dmu/N = k1*g + k2*(h - mean) + k3
+//   d mhat_c = alpha_c*gamma_c*G_c ; du_c = tinv*(dmhat_c - mhat_c*sum(dmhat*mhat)/(C-1)) ;
+//   dmu_c = du_c - mean_c(du)
+//   dgamma += Gx + alpha*mhat*G ; dbeta += G ; dalpha += gamma*mhat*G
+__global__ __launch_bounds__(1024) void inpp_bwd_finalize_kernel(const float2* __restrict__ part, int ngrp, float N,
+                                                                 const float4* __restrict__ nst,
+                                                                 const float* __restrict__ alpha,
+                                                                 const float* __restrict__ gamma, int B, int C,
+                                                                 float4* __restrict__ coef, float* __restrict__ dalpha,
+                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ double r0[1024], r1[1024];
+  const int tid = threadIdx.x, Gt = 1024 / C, gi = tid / C, c = tid % C;
+  double acc_a = 0.0, acc_g = 0.0, acc_b = 0.0;
+  for (int b = 0; b < B; ++b) {
+    double s0 = 0.0, s1 = 0.0;
+    for (int k = gi; k < ngrp; k += Gt) {
+      const float2 v = part[((size_t)b * ngrp + k) * C + c];
+      s0 += v.x;
+      s1 += v.y;
+    }
+    r0[tid] = s0;
+    r1[tid] = s1;
+    __syncthreads();
+    if (gi == 0) {
+      for (int k = 1; k < Gt; ++k) {
+        s0 += r0[k * C + c];
+        s1 += r1[k * C + c];
+      }
+    }
+    __syncthreads();
+    const float4 ns = nst[(size_t)b * C + c];   // mean, rstd, mhat, tinv
+    const double Gc = s0, Gx = s1;
+    const double al = alpha[c], gm = gamma[c];
+    const double dmh = al * gm * Gc;
+    if (gi == 0) {
+      r0[c] = dmh * ns.z;
+    }
+    __syncthreads();
+    for (int s = C / 2; s > 0; s >>= 1) {
+      if (gi == 0 && c < s) r0[c] += r0[c + s];
+      __syncthreads();
+    }
+    const double A = r0[0];
+    __syncthreads();
+    const double du = (double)ns.w * (dmh - (double)ns.z * A / (C - 1));
+    if (gi == 0) r1[c] = du;
+    __syncthreads();
+    for (int s = C / 2; s > 0; s >>= 1) {
+      if (gi == 0 && c < s) r1[c] += r1[c + s];
+      __syncthreads();
+    }
+    const double dmu = du - r1[0] / C;
+    __syncthreads();
+    if (gi == 0) {
+      const double rs = ns.y, mu = ns.x;
+      // dh = k1*g + k2*(h - mean) + k3: centring h before the product keeps the cancellation
+      // between the xhat and mean terms out of float32
+      const double k1 = gm * rs;
+      const double k2 = -gm * rs * rs * Gx / N;
+      const double k3 = -gm * rs * Gc / N + dmu / N;
+      coef[(size_t)b * C + c] = make_float4((float)k1, (float)k2, (float)k3, (float)mu);
+      acc_g += Gx + al * (double)ns.z * Gc;
+      acc_b += Gc;
+      acc_a += gm * (double)ns.z * Gc;
+    }
+  }
+  if (gi == 0) {
+    dalpha[c] = (float)acc_a;
+    dgamma[c] = (float)acc_g;
+    dbeta[c] = (float)acc_b;
+  }
+}
+
+// out = k1*g + k2*(h - mean) + k3 (+ r1) (+ r2)
+__global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ h,
+                                                             const float4* __restrict__ coef, const float* r1,
+                                                             const float* r2, float* out, int HW, int C, size_t n4) {
+  const int C4 = C / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const size_t b = i / C4 / HW;
+    const float4* cf = coef + b * C + c;
+    const float4 k0 = cf[0], kk1 = cf[1], kk2 = cf[2], kk3 = cf[3];
+    const float4 gv = reinterpret_cast<const float4*>(g)[i], hv = reinterpret_cast<const float4*>(h)[i];
+    float4 v = make_float4(fmaf(k0.x, gv.x, fmaf(k0.y, hv.x - k0.w, k0.z)), fmaf(kk1.x, gv.y, fmaf(kk1.y, hv.y - kk1.w, kk1.z)),
+                           fmaf(kk2.x, gv.z, fmaf(kk2.y, hv.z - kk2.w, kk2.z)), fmaf(kk3.x, gv.w, fmaf(kk3.y, hv.w - kk3.w, kk3.z)));
+    if (r1) {
+      const float4 t = reinterpret_cast<const float4*>(r1)[i];
+      v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
+    }
+    if (r2) {
+      const float4 t = reinterpret_cast<const float4*>(r2)[i];
+      v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
+    }
+    reinterpret_cast<float4*>(out)[i] = v;
+  }
+}
+
+static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 256 * 32); }
+
+hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
+                         int HW, int C, float* part, float* coef, float* dalpha, float* dgamma, float* dbeta,
+                         const float* r1, const float* r2, float* out, hipStream_t st) {
+  if (HW % 512 || C % 4 || C > 1024 || (256 % (C / 4))) return hipErrorInvalidValue;
+  const int ngrp = HW / 512;
+  hipLaunchKernelGGL(inpp_bwd_reduce_kernel, dim3(ngrp, B), dim3(256), 0, st, g, h,
+                     reinterpret_cast<const float4*>(nst), reinterpret_cast<float2*>(part), HW, C);
+  hipLaunchKernelGGL(inpp_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, reinterpret_cast<const float2*>(part), ngrp,
+                     (float)HW, reinterpret_cast<const float4*>(nst), alpha, gamma, B, C,
+                     reinterpret_cast<float4*>(coef), dalpha, dgamma, dbeta);
+  const size_t n4 = (size_t)B * HW * C / 4;
+  hipLaunchKernelGGL(inpp_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, h,
+                     reinterpret_cast<const float4*>(coef), r1, r2, out, HW, C, n4);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- pooling / upsampling adjoints
+// ConvMeanPool: out = (o00 + o10 + o01 + o11)/4 -> d o_yx = dout[y/2][x/2] / 4   (dst full-res)
+__global__ void unpool_kernel(const float* __restrict__ dout, float* __restrict__ dst, int H, int W, int C, size_t n4) {
+  const int C4 = C / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    size_t p = i / C4;
+    const int x = p % W;
+    p /= W;
+    const int y = p % H;
+    const size_t b = p / H;
+    const float4 v = reinterpret_cast<const float4*>(dout)[((b * (H / 2) + y / 2) * (W / 2) + x / 2) * C4 + c4];
+    reinterpret_cast<float4*>(dst)[i] = make_float4(v.x * 0.25f, v.y * 0.25f, v.z * 0.25f, v.w * 0.25f);
+  }
+}
+
+// argmax (0..24, row-major window order, first max wins as torch's max_pool2d) of every 5x5 window
+__global__ void maxpool5_argmax_kernel(const float* __restrict__ in, uint8_t* __restrict__ idx, int H, int W, int C,
+                                       size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = i % C;
+    size_t p = i / C;
+    const int x = p % W;
+    p /= W;
+    const int y = p % H;
+    const size_t b = p / H;
+    float m = -INFINITY;
+    int best = 12;
+    for (int dy = -2; dy <= 2; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= H) continue;
+      for (int dx = -2; dx <= 2; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= W) continue;
+        const float v = in[((b * H + yy) * W + xx) * C + c];
+        if (v > m || v != v) {
+          m = v;
+          best = (dy + 2) * 5 + dx + 2;
+        }
+      }
+    }
+    idx[i] = (uint8_t)best;
+  }
+}
+
+// dst[q] = (res ? res[q] : 0) + sum over windows p containing q whose argmax is q of dp[p]
+__global__ void maxpool5_bwd_kernel(const float* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                    const float* __restrict__ res, float* __restrict__ dst, int H, int W, int C, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = i % C;
+    size_t p = i / C;
+    const int x = p % W;
+    p /= W;
+    const int y = p % H;
+    const size_t b = p / H;
+    float s = 0.f;
+    for (int dy = -2; dy <= 2; ++dy) {       // window centre (y+dy, x+dx); q sits at offset (-dy, -dx)
+      const int yy = y + dy;
+      if (yy < 0 || yy >= H) continue;
+      for (int dx = -2; dx <= 2; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= W) continue;
+        const size_t j = ((b * H + yy) * W + xx) * C + c;
+        if (idx[j] == (2 - dy) * 5 + (2 - dx)) s += dp[j];
+      }
+    }
+    dst[i] = res ? res[i] + s : s;
+  }
+}
+
+// adjoint of the bilinear align_corners upsample [h][w] -> [H][W] (forward: conv epilogue `up`):
+// dlow[i][j] += sum_{y,x} wy(y,i) wx(x,j) g[y][x]  (gather over the few y, x that reach (i, j))
+SDP_DEV void up_weights(int o, int n_lo, float scale, int* i0, int* i1, float* w0, float* w1) {
+  const float f = scale * (float)o;
+  const int a = (int)f;
+  const int ap = a < n_lo - 1 ? 1 : 0;
+  *i0 = a;
+  *i1 = a + ap;
+  *w1 = f - (float)a;
+  *w0 = 1.f - *w1;
+}
+
+__global__ void upsample_bwd_kernel(const float* __restrict__ g, float* __restrict__ dlow, int H, int W, int C,
+                                    int accumulate, size_t n4) {
+  const int h = H / 2, w = W / 2, C4 = C / 4;
+  const float sh = (float)(h - 1) / (float)(H - 1), sw = (float)(w - 1) / (float)(W - 1);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    size_t p = i / C4;
+    const int j = p % w;
+    p /= w;
+    const int ii = p % h;
+    const size_t b = p / h;
+    // high-res rows whose source rows include ii: scale*y in (ii-1, ii+1]
+    const int ylo = max(0, (int)floorf((float)(ii - 1) / sh) - 1), yhi = min(H - 1, (int)ceilf((float)(ii + 1) / sh) + 1);
+    const int xlo = max(0, (int)floorf((float)(j - 1) / sw) - 1), xhi = min(W - 1, (int)ceilf((float)(j + 1) / sw) + 1);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int y = ylo; y <= yhi; ++y) {
+      int a0, a1;
+      float u0, u1;
+      up_weights(y, h, sh, &a0, &a1, &u0, &u1);
+      const float wy = (a0 == ii ? u0 : 0.f) + (a1 == ii ? u1 : 0.f);
+      if (wy == 0.f) continue;
+      for (int x = xlo; x <= xhi; ++x) {
+        int b0, b1;
+        float v0, v1;
+        up_weights(x, w, sw, &b0, &b1, &v0, &v1);
+        const float wx = (b0 == j ? v0 : 0.f) + (b1 == j ? v1 : 0.f);
+        if (wx == 0.f) continue;
+        const float4 gv = reinterpret_cast<const float4*>(g)[((b * H + y) * W + x) * C4 + c4];
+        const float ww = wy * wx;
+        s = make_float4(fmaf(ww, gv.x, s.x), fmaf(ww, gv.y, s.y), fmaf(ww, gv.z, s.z), fmaf(ww, gv.w, s.w));
+      }
+    }
+    float4* o = reinterpret_cast<float4*>(dlow) + i;
+    if (accumulate) {
+      const float4 t = *o;
+      s = make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
+    }
+    *o = s;
+  }
+}
+
+// dst = dy * elu'(from the ELU output y) (+ res)
+__global__ void elu_bwd_post_kernel(const float* __restrict__ dy, const float* __restrict__ y, const float* res,
+                                    float* dst, size_t n4) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 d = reinterpret_cast<const float4*>(dy)[i], yv = reinterpret_cast<const float4*>(y)[i];
+    float4 v = make_float4(d.x * elu_grad(yv.x, 2), d.y * elu_grad(yv.y, 2), d.z * elu_grad(yv.z, 2),
+                           d.w * elu_grad(yv.w, 2));
+    if (res) {
+      const float4 t = reinterpret_cast<const float4*>(res)[i];
+      v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
+    }
+    reinterpret_cast<float4*>(dst)[i] = v;
+  }
+}
+
+// dst = a + b (float4 lanes)
+__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* dst, size_t n4) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const float4 x = reinterpret_cast<const float4*>(a)[i], y = reinterpret_cast<const float4*>(b)[i];
+    reinterpret_cast<float4*>(dst)[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  }
+}
+
+// bias gradient: part[blk][c] = sum over the block's pixels ; then out[c] = sum_blk part
+__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ dy, size_t npix, int C,
+                                                       float* __restrict__ part) {
+  __shared__ float red[256 * 4];
+  const int C4 = C / 4, PL = 256 / C4, tid = threadIdx.x, c4 = tid % C4, pl = tid / C4;
+  const size_t per = (npix + gridDim.x - 1) / gridDim.x;
+  const size_t p0 = blockIdx.x * per, p1 = min(npix, p0 + per);
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (size_t p = p0 + pl; p < p1; p += PL) {
+    const float4 v = *reinterpret_cast<const float4*>(dy + p * C + c4 * 4);
+    s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) red[(pl * C4 + c4) * 4 + k] = s[k];
+  __syncthreads();
+  for (int i = tid; i < C; i += 256) {
+    float a = 0.f;
+    for (int k = 0; k < PL; ++k) a += red[(k * C4 + i / 4) * 4 + (i & 3)];
+    part[(size_t)blockIdx.x * C + i] = a;
+  }
+}
+
+// out[i] = sum_k part[k*stride + i] (fixed order, f64) ; n outputs, K partial rows
+__global__ void sum_rows_kernel(const float* __restrict__ part, int K, int n, int stride, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int k = 0; k < K; ++k) s += part[(size_t)k * stride + i];
+  out[i] = (float)s;
+}
+
+static hipError_t sum_rows(const float* part, int K, int n, int stride, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, part, K, n, stride, out);
+  return hipGetLastError();
+}
+
+hipError_t chan_sum(const float* dy, size_t npix, int C, float* part, float* out, hipStream_t st) {
+  if (C % 4 || 256 % (C / 4)) return hipErrorInvalidValue;
+  const int nb = 256;
+  hipLaunchKernelGGL(chan_sum_kernel, dim3(nb), dim3(256), 0, st, dy, npix, C, part);
+  return sum_rows(part, nb, C, C, out, st);
+}
+
+hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hipStream_t st) {
+  const size_t n4 = (size_t)B * H * W * C / 4;
+  hipLaunchKernelGGL(unpool_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dout, dst, H, W, C, n4);
+  return hipGetLastError();
+}
+
+hipError_t maxpool5_backward(const float* src, const float* dp, const float* res, float* dst, uint8_t* idx, int B, int H,
+                             int W, int C, hipStream_t st) {
+  const size_t n = (size_t)B * H * W * C;
+  hipLaunchKernelGGL(maxpool5_argmax_kernel, dim3(grid_for(n)), dim3(256), 0, st, src, idx, H, W, C, n);
+  hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, dp, idx, res, dst, H, W, C, n);
+  return hipGetLastError();
+}
+
+hipError_t upsample_backward(const float* g, float* dlow, int B, int H, int W, int C, int accumulate, hipStream_t st) {
+  const size_t n4 = (size_t)B * (H / 2) * (W / 2) * C / 4;
+  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, dlow, H, W, C, accumulate, n4);
+  return hipGetLastError();
+}
+
+hipError_t elu_backward_post(const float* dy, const float* y, const float* res, float* dst, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(elu_bwd_post_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, dy, y, res, dst, n / 4);
+  return hipGetLastError();
+}
+
+hipError_t add_tensors(const float* a, const float* b, float* dst, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(add_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a, b, dst, n / 4);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- begin_conv weight gradient
+// dW[co][ci][tap] = sum_p dx0[p][co] * in4[p + tap - (1,1)][ci] (zero pad), db[co] = sum_p dx0[p][co]
+// in4 = (2x-1, 2x-1, linspace W, linspace H) (ncsnv2.py:485-496).  Block: ROWS rows x 64 px.
+SDP_DEV float linspace01_t(int i, int n) {
+  if (n == 1) return 0.f;
+  const float step = 1.0f / (float)(n - 1);
+  return i < n / 2 ? step * (float)i : 1.0f - step * (float)(n - 1 - i);
+}
+
+constexpr int BW_ROWS = 8;
+__global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                          float* __restrict__ part, int H, int W) {
+  __shared__ float sp[4][3][66];
+  __shared__ float sd[64][129];
+  const int tid = threadIdx.x, co = tid & 127, half = tid >> 7;
+  const int tiles_row = W / 64, rows_blk = H / BW_ROWS;
+  const int per_img = rows_blk * tiles_row;
+  const int b = blockIdx.x / per_img, t = blockIdx.x % per_img;
+  const int y0 = (t / tiles_row) * BW_ROWS, x0 = (t % tiles_row) * 64;
+  float acc[18];
+#pragma unroll
+  for (int k = 0; k < 18; ++k) acc[k] = 0.f;
+  float db = 0.f;
+  for (int r = 0; r < BW_ROWS; ++r) {
+    const int y = y0 + r;
+    __syncthreads();
+    for (int i = tid; i < 4 * 3 * 66; i += 256) {
+      const int ci = i / 198, rr = (i / 66) % 3, c = i % 66;
+      const int yy = y - 1 + rr, xx = x0 - 1 + c;
+      float v = 0.f;
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        if (ci < 2) v = 2.f * x[(((size_t)b * 2 + ci) * H + yy) * W + xx] - 1.f;
+        else if (ci == 2) v = linspace01_t(xx, W);
+        else v = linspace01_t(yy, H);
+      }
+      sp[ci][rr][c] = v;
+    }
+    for (int i = tid; i < 64 * 32; i += 256) {
+      const int px = i >> 5, c4 = i & 31;
+      const float4 v = *reinterpret_cast<const float4*>(dy + (((size_t)b * H + y) * W + x0 + px) * 128 + c4 * 4);
+      sd[px][c4 * 4] = v.x; sd[px][c4 * 4 + 1] = v.y; sd[px][c4 * 4 + 2] = v.z; sd[px][c4 * 4 + 3] = v.w;
+    }
+    __syncthreads();
+    for (int px = 0; px < 64; ++px) {
+      const float g = sd[px][co];
+      if (half == 0) db += g;
+#pragma unroll
+      for (int k = 0; k < 18; ++k) {
+        const int j = half * 18 + k, ci = j / 9, tap = j % 9;
+        acc[k] = fmaf(g, sp[ci][tap / 3][px + tap % 3], acc[k]);
+      }
+    }
+  }
+  float* o = part + (size_t)blockIdx.x * (128 * 37);
+#pragma unroll
+  for (int k = 0; k < 18; ++k) o[co * 36 + half * 18 + k] = acc[k];
+  if (half == 0) o[128 * 36 + co] = db;
+}
+
+hipError_t begin_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int H, int W,
+                            hipStream_t st) {
+  if (H % BW_ROWS || W % 64) return hipErrorInvalidValue;
+  const int nb = B * (H / BW_ROWS) * (W / 64);
+  hipLaunchKernelGGL(begin_wgrad_kernel, dim3(nb), dim3(256), 0, st, x, dy, part, H, W);
+  (void)sum_rows(part, nb, 128 * 36, 128 * 37, dw, st);
+  return sum_rows(part + 128 * 36, nb, 128, 128 * 37, db, st);
+}
+
+// ---------------------------------------------------------------- end_conv backward
+// Forward (ncsnv2.py:510-516): out[b][co] = (conv3x3_zero(ELU(IN++(o)), W) + bias) / sigmas[y_b].
+// dend = dscore / sigmas[y_b].  Data gradient (to the ELU output) with the IN++/ELU derivative
+// applied (g = da * elu'(o*scale + shift)); weight and bias gradients.
+__global__ __launch_bounds__(256) void end_dgrad_kernel(const float* __restrict__ dscore, const float* __restrict__ sigmas,
+                                                        const int64_t* __restrict__ labels, const float* __restrict__ w,
+                                                        const float* __restrict__ o, const float* __restrict__ ss,
+                                                        float* __restrict__ g, int H, int W) {
+  constexpr int C = 128;
+  __shared__ float sd[2][3][66];
+  __shared__ float sw[2 * C * 9];
+  const int tid = threadIdx.x;
+  const int tiles_row = W / 64, per_img = H * tiles_row;
+  const int b = blockIdx.x / per_img, t = blockIdx.x % per_img;
+  const int y = t / tiles_row, x0 = (t % tiles_row) * 64;
+  const float inv = 1.f / sigmas[labels[b]];
+  for (int i = tid; i < 2 * 3 * 66; i += 256) {
+    const int co = i / 198, rr = (i / 66) % 3, c = i % 66;
+    const int yy = y - 1 + rr, xx = x0 - 1 + c;
+    sd[co][rr][c] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? dscore[(((size_t)b * 2 + co) * H + yy) * W + xx] * inv : 0.f;
+  }
+  for (int i = tid; i < 2 * C * 9; i += 256) sw[i] = w[i];
+  __syncthreads();
+  const int c4 = tid & 31, pl = tid >> 5;
+  const float* ssb = ss + ((size_t)b * C + c4 * 4) * 2;
+  const float4 s0 = *reinterpret_cast<const float4*>(ssb), s1 = *reinterpret_cast<const float4*>(ssb + 4);
+  for (int px = pl; px < 64; px += 8) {
+    float da[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int co = 0; co < 2; ++co)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int kh = tap / 3, kw = tap % 3;
+        const float dv = sd[co][2 - kh][px + 2 - kw];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) da[k] = fmaf(dv, sw[(co * C + c4 * 4 + k) * 9 + tap], da[k]);
+      }
+    const size_t idx = (((size_t)b * H + y) * W + x0 + px) * C + c4 * 4;
+    const float4 h = *reinterpret_cast<const float4*>(o + idx);
+    const float z0 = fmaf(h.x, s0.x, s0.y), z1 = fmaf(h.y, s0.z, s0.w), z2 = fmaf(h.z, s1.x, s1.y), z3 = fmaf(h.w, s1.z, s1.w);
+    *reinterpret_cast<float4*>(g + idx) =
+        make_float4(da[0] * elu_grad(z0, 1), da[1] * elu_grad(z1, 1), da[2] * elu_grad(z2, 1), da[3] * elu_grad(z3, 1));
+  }
+}
+
+constexpr int EW_ROWS = 8;
+__global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict__ dscore, const float* __restrict__ sigmas,
+                                                        const int64_t* __restrict__ labels, const float* __restrict__ o,
+                                                        const float* __restrict__ ss, float* __restrict__ part, int H,
+                                                        int W) {
+  constexpr int C = 128;
+  __shared__ float sp[3 * 34 * C];
+  __shared__ float sd[2][32];
+  const int tid = threadIdx.x, ci = tid >> 1, co = tid & 1;
+  const int tiles_row = W / 32, per_img = (H / EW_ROWS) * tiles_row;
+  const int b = blockIdx.x / per_img, t = blockIdx.x % per_img;
+  const int y0 = (t / tiles_row) * EW_ROWS, x0 = (t % tiles_row) * 32;
+  const float inv = 1.f / sigmas[labels[b]];
+  const float* ssb = ss + (size_t)b * C * 2;
+  float acc[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+  float db = 0.f;
+  for (int r = 0; r < EW_ROWS; ++r) {
+    const int y = y0 + r;
+    __syncthreads();
+    for (int i = tid; i < 3 * 34 * 32; i += 256) {
+      const int pix = i >> 5, c4 = i & 31, rr = pix / 34, cc = pix % 34;
+      const int yy = y - 1 + rr, xx = x0 - 1 + cc;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        const float4 h = *reinterpret_cast<const float4*>(o + (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(ssb + c4 * 8), s1 = *reinterpret_cast<const float4*>(ssb + c4 * 8 + 4);
+        v = make_float4(elu(fmaf(h.x, s0.x, s0.y)), elu(fmaf(h.y, s0.z, s0.w)), elu(fmaf(h.z, s1.x, s1.y)),
+                        elu(fmaf(h.w, s1.z, s1.w)));
+      }
+      *reinterpret_cast<float4*>(&sp[pix * C + c4 * 4]) = v;
+    }
+    if (tid < 64) {
+      const int c2 = tid >> 5, px = tid & 31;
+      sd[c2][px] = dscore[(((size_t)b * 2 + c2) * H + y) * W + x0 + px] * inv;
+    }
+    __syncthreads();
+    for (int px = 0; px < 32; ++px) {
+      const float gv = sd[co][px];
+      if (ci == 0) db += gv;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) acc[tap] = fmaf(gv, sp[((tap / 3) * 34 + px + tap % 3) * C + ci], acc[tap]);
+    }
+  }
+  float* op = part + (size_t)blockIdx.x * (2 * C * 9 + 2);
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) op[(co * C + ci) * 9 + tap] = acc[tap];
+  if (ci == 0) op[2 * C * 9 + co] = db;
+}
+
+hipError_t end_conv_backward(const float* dscore, const float* sigmas, const int64_t* labels, const float* w,
+                             const float* o, const float* ss, float* g, float* part, float* dw, float* db, int B, int H,
+                             int W, hipStream_t st) {
+  if (H % EW_ROWS || W % 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(end_dgrad_kernel, dim3(B * H * (W / 64)), dim3(256), 0, st, dscore, sigmas, labels, w, o, ss, g, H, W);
+  const int nb = B * (H / EW_ROWS) * (W / 32);
+  hipLaunchKernelGGL(end_wgrad_kernel, dim3(nb), dim3(256), 0, st, dscore, sigmas, labels, o, ss, part, H, W);
+  (void)sum_rows(part, nb, 2 * 128 * 9, 2 * 128 * 9 + 2, dw, st);
+  return sum_rows(part + 2 * 128 * 9, nb, 2, 2 * 128 * 9 + 2, db, st);
+}
+
+// ---------------------------------------------------------------- DSM loss (losses/dsm.py:67-119)
+// target = -noise / sigma_b^2 ; r = mask * (score - target) ; numPixels = sum(mask) (whole batch)
+// loss_b = 0.5 * sum(r^2) * CHW / numPixels * sigma_b^p ; loss = mean_b ; dscore = d loss / d score
+constexpr int DSM_BLK = 64;   // blocks per image
+__global__ __launch_bounds__(256) void dsm_mask_sum_kernel(const float* __restrict__ mask, int n_img, float* part) {
+  __shared__ float red[4];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const float* m = mask + (size_t)b * n_img;
+  float s = 0.f;
+  for (int i = blockIdx.x * 256 + tid; i < n_img; i += DSM_BLK * 256) s += m[i];
+  s = wsum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) part[b * DSM_BLK + blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void dsm_grad_kernel(const float* __restrict__ score, const float* __restrict__ noise,
+                                                       const float* __restrict__ mask, const float* __restrict__ used_sigma,
+                                                       const float* __restrict__ mpart, int B, int n_img, float power,
+                                                       float* __restrict__ dscore, float* __restrict__ lpart) {
+  __shared__ double red[4];
+  const int b = blockIdx.y, tid = threadIdx.x;
+  double np = 0.0;
+  for (int k = 0; k < B * DSM_BLK; ++k) np += mpart[k];
+  const float sg = used_sigma[b];
+  const float inv2 = 1.f / (sg * sg);
+  const double scale = (double)n_img / np * pow((double)sg, (double)power) / B;
+  const size_t base = (size_t)b * n_img;
+  double s = 0.0;
+  for (int i = blockIdx.x * 256 + tid; i < n_img; i += DSM_BLK * 256) {
+    const float m = mask[base + i];
+    const float tgt = -inv2 * noise[base + i];
+    const float r = m * (score[base + i] - tgt);
+    s += (double)r * r;
+    dscore[base + i] = (float)(scale * (double)(m * r));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  if (tid == 0) lpart[b * DSM_BLK + blockIdx.x] = (float)(red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ void dsm_final_kernel(const float* __restrict__ mpart, const float* __restrict__ lpart,
+                                 const float* __restrict__ used_sigma, int B, int n_img, float power, float* loss,
+                                 float* loss_per) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double np = 0.0;
+  for (int k = 0; k < B * DSM_BLK; ++k) np += mpart[k];
+  double tot = 0.0;
+  for (int b = 0; b < B; ++b) {
+    double s = 0.0;
+    for (int k = 0; k < DSM_BLK; ++k) s += lpart[b * DSM_BLK + k];
+    const double lb = 0.5 * s * n_img / np * pow((double)used_sigma[b], (double)power);
+    if (loss_per) loss_per[b] = (float)lb;
+    tot += lb;
+  }
+  *loss = (float)(tot / B);
+}
+
+hipError_t dsm_loss(const float* score, const float* noise, const float* mask, const float* used_sigma, int B, int n_img,
+                    float power, float* dscore, float* loss, float* loss_per, float* part, hipStream_t st) {
+  float* mpart = part;
+  float* lpart = part + B * DSM_BLK;
+  hipLaunchKernelGGL(dsm_mask_sum_kernel, dim3(DSM_BLK, B), dim3(256), 0, st, mask, n_img, mpart);
+  hipLaunchKernelGGL(dsm_grad_kernel, dim3(DSM_BLK, B), dim3(256), 0, st, score, noise, mask, used_sigma, mpart, B, n_img,
+                     power, dscore, lpart);
+  hipLaunchKernelGGL(dsm_final_kernel, dim3(1), dim3(64), 0, st, mpart, lpart, used_sigma, B, n_img, power, loss, loss_per);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- Adam + EMA
+// torch.optim.Adam (weight_decay 0, amsgrad off):
+//   m = m + (1-b1)(g - m) ; v = b2 v + (1-b2) g^2 ; p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)
+// EMAHelper.update: shadow = (1-mu) p + mu shadow
+__global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                float* __restrict__ v, float* __restrict__ shadow, size_t n, float b1, float b2,
+                                float eps, float step_size, float bc2_sqrt, float mu) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float gi = g[i];
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    const float pi = p[i] - step_size * (mi / denom);
+    p[i] = pi;
+    if (shadow) shadow[i] = (1.f - mu) * pi + mu * shadow[i];
+  }
+}
+
+hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow, size_t n, float b1, float b2, float eps,
+                    float step_size, float bc2_sqrt, float mu, hipStream_t st) {
+  hipLaunchKernelGGL(adam_ema_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, shadow, n, b1, b2, eps, step_size,
+                     bc2_sqrt, mu);
+  return hipGetLastError();
+}
+
+}  // namespace sdp

@@ -1,0 +1,274 @@
+// Weight gradient of the score network's 3x3 / dilated / 1x1 convolutions on MFMA (gfx950),
+// for the DSM training backward (LiDARGen/losses/dsm.py:67-119 -> loss.backward(),
+// runners/ncsn_runner_kitti_simultaneous.py:229-232).
+//
+//   dW[co][ci][kh][kw] = sum_{b,y,x} dy[b][y][x][co] * a[b][y + (kh-1)d][x + (kw-1)d][ci]
+//   a = prologue(in): the forward conv's input transform (InstanceNorm++ affine + ELU, ELU,
+//       or none), zero or circular padding.
+//
+// GEMM view per tap: M = Cout, N = Cin, K = pixels.  Both operands sit in HBM as NHWC
+// (channel-contiguous), but an MFMA lane needs 8 consecutive K (= pixels) of one channel, so
+// the tiles are staged in LDS as [pixel][32 channels] bf16 rows (64 B, conflict-free) and read
+// with ds_read_b64_tr_b16, the CDNA4 transposing LDS read: a tap's pixel shift is then just a
+// row offset, and the 9 taps reuse one staged input patch.
+//
+// Workgroup (4 waves, one per SIMD): 128 Cout x 32 Cin x all taps; wave w owns Cout
+// [32w, 32w+32) -> 9 accumulators of 32x32.  Grid (split, Cin/32, Cout/128): the pixels are
+// split S ways, every workgroup walks its range of TR x TC pixel tiles (polyphase sub-grid
+// for dilated convs, like the forward) with the next tile's global loads in registers, and
+// writes its partial sums to part[split][tap][Cout][Cin]; conv_wgrad_reduce sums the splits
+// in a fixed order (deterministic) into the state_dict layout [Cout][Cin][k][k].
+#include "common.h"
+#include "kernels.h"
+
+namespace sdp {
+
+typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 vbf16x4;
+typedef __attribute__((address_space(3))) vbf16x4 lds_vbf16x4;
+
+SDP_DEV bf16x4 ds_read_tr(const char* p) {
+  const vbf16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      reinterpret_cast<lds_vbf16x4*>(reinterpret_cast<uintptr_t>(p)));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+SDP_DEV bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  bf16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+
+template <int TC, int KS>
+struct WgTile {
+  static constexpr int TR = 128 / TC;
+  static constexpr int HALO = KS == 3 ? 1 : 0;
+  static constexpr int PC = TC + 2 * HALO, PR = TR + 2 * HALO, NPIX = PR * PC;
+  static constexpr int NUA = (NPIX * 8 + 255) / 256;   // a-patch float4 units per thread
+  static constexpr int NUD = 16;                        // dy tile: 128 px x 128 co / 4 / 256
+  static constexpr int DY_PLANE = 4 * 128 * 64;         // [wave][px][32 co] bf16
+  static constexpr int A_PLANE = NPIX * 64;             // [px][32 ci] bf16
+};
+
+template <int MODE, int TC, int KS>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  using T = WgTile<TC, KS>;
+  constexpr int NT = KS * KS;
+  constexpr int NPL = MODE == MODE_F32X3 ? 2 : 1;      // bf16 planes: hi (+ lo)
+  __shared__ __attribute__((aligned(16))) char lds[NPL * (T::DY_PLANE + T::A_PLANE)];
+  char* const dyL = lds;                                // plane pl at + pl * DY_PLANE
+  char* const aL = lds + NPL * T::DY_PLANE;             // plane pl at + pl * A_PLANE
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
+  const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c, tiles_img = tiles_rc * d * d;
+  const int total = a.B * tiles_img;
+  const int split = blockIdx.x, S = gridDim.x;
+  const int t_begin = (int)((long long)total * split / S), t_end = (int)((long long)total * (split + 1) / S);
+  const int ci0 = blockIdx.y * 32, co0 = blockIdx.z * 128;
+  const int Cin = a.Cin, Cout = a.Cout;
+
+  f32x16 acc[NT];
+  static_for<0, NT>([&](auto i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  });
+
+  float4 rd[T::NUD], ra[T::NUA];
+  int tb = 0, tph_r = 0, tph_c = 0, tsr0 = 0, tsc0 = 0;
+  auto decode = [&](int t) {
+    tb = t / tiles_img;
+    int r = t - tb * tiles_img;
+    const int ph = r / tiles_rc;
+    r -= ph * tiles_rc;
+    tph_r = ph / d;
+    tph_c = ph - tph_r * d;
+    tsr0 = (r / tiles_c) * T::TR;
+    tsc0 = (r % tiles_c) * TC;
+  };
+  // global -> registers for tile t (decoded into tb, tph_*, tsr0, tsc0)
+  auto load_tile = [&]() {
+    const float* dyb = a.dy + (size_t)tb * a.H * a.W * Cout + co0;
+#pragma unroll
+    for (int k = 0; k < T::NUD; ++k) {
+      const int u = tid + k * 256, px = u >> 5, cv = u & 31;
+      const int y = (tsr0 + px / TC) * d + tph_r, x = (tsc0 + px % TC) * d + tph_c;
+      rd[k] = *reinterpret_cast<const float4*>(dyb + ((size_t)y * a.W + x) * Cout + cv * 4);
+    }
+    const float* inb = a.in + (size_t)tb * a.H * a.W * Cin + ci0;
+#pragma unroll
+    for (int k = 0; k < T::NUA; ++k) {
+      int u = tid + k * 256;
+      u = u < T::NPIX * 8 ? u : 0;
+      const int pix = u >> 3, cv = u & 7;
+      int sr = tsr0 - T::HALO + pix / T::PC, sc = tsc0 - T::HALO + pix % T::PC;
+      if (a.circular) {
+        sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
+        sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
+      } else {
+        sr = min(max(sr, 0), Hs - 1);
+        sc = min(max(sc, 0), Ws - 1);
+      }
+      const int y = sr * d + tph_r, x = sc * d + tph_c;
+      ra[k] = *reinterpret_cast<const float4*>(inb + ((size_t)y * a.W + x) * Cin + cv * 4);
+    }
+  };
+  auto put_bf16 = [&](char* base, int plane, int off, float4 v) {
+    bf16x4 hi;
+    hi[0] = (__bf16)v.x; hi[1] = (__bf16)v.y; hi[2] = (__bf16)v.z; hi[3] = (__bf16)v.w;
+    *reinterpret_cast<bf16x4*>(base + off) = hi;
+    if constexpr (MODE == MODE_F32X3) {
+      bf16x4 lo;
+      lo[0] = (__bf16)(v.x - (float)hi[0]);
+      lo[1] = (__bf16)(v.y - (float)hi[1]);
+      lo[2] = (__bf16)(v.z - (float)hi[2]);
+      lo[3] = (__bf16)(v.w - (float)hi[3]);
+      *reinterpret_cast<bf16x4*>(base + plane + off) = lo;
+    }
+  };
+  // registers -> LDS (prologue transform on the input patch, zero padding, bf16 split)
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int k = 0; k < T::NUD; ++k) {
+      const int u = tid + k * 256, px = u >> 5, cv = u & 31;
+      put_bf16(dyL, T::DY_PLANE, (cv >> 3) * (128 * 64) + px * 64 + (cv & 7) * 8, rd[k]);
+    }
+    const float* ssb = a.pro_ss + (size_t)tb * a.ss_bstride + ci0 * 2;
+#pragma unroll
+    for (int k = 0; k < T::NUA; ++k) {
+      const int u = tid + k * 256;
+      if (u >= T::NPIX * 8) break;
+      const int pix = u >> 3, cv = u & 7;
+      float4 v = ra[k];
+      if (a.pro_mode != PRO_NONE) {
+        const float4 s0 = *reinterpret_cast<const float4*>(ssb + cv * 8);
+        const float4 s1 = *reinterpret_cast<const float4*>(ssb + cv * 8 + 4);
+        v = make_float4(fmaf(v.x, s0.x, s0.y), fmaf(v.y, s0.z, s0.w), fmaf(v.z, s1.x, s1.y), fmaf(v.w, s1.z, s1.w));
+        v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
+      }
+      if (!a.circular && KS == 3) {
+        const int sr = tsr0 - 1 + pix / T::PC, sc = tsc0 - 1 + pix % T::PC;
+        if (sr < 0 || sr >= Hs || sc < 0 || sc >= Ws) v = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      put_bf16(aL, T::A_PLANE, pix * 64 + cv * 8, v);
+    }
+  };
+
+  // transposed-read lane roles (ds_read_b64_tr_b16, 32x32x16 operand): lane l of 16-lane
+  // group G supplies row q = (l & 15) >> 2 (K), columns 4p .. 4p+3, p = l & 3 (M or N)
+  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int kq = 8 * (G >> 1) + q;                      // K of this lane's address, read r adds 4r
+  const int mcol = 16 * (G & 1) + 4 * p;                 // channel of this lane's address
+  const char* dy_rd = dyL + wave * (128 * 64) + mcol * 2;
+  const char* a_rd = aL + mcol * 2;
+
+  if (t_begin < t_end) {
+    decode(t_begin);
+    load_tile();
+  }
+  for (int t = t_begin; t < t_end; ++t) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (t + 1 < t_end) {
+      decode(t + 1);
+      load_tile();
+    }
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {   // 16 pixels per k step
+      const int k0 = 16 * s + kq, k1 = k0 + 4;
+      bf16x8 ahi = cat8(ds_read_tr(dy_rd + k0 * 64), ds_read_tr(dy_rd + k1 * 64)), alo;
+      if constexpr (MODE == MODE_F32X3)
+        alo = cat8(ds_read_tr(dy_rd + T::DY_PLANE + k0 * 64), ds_read_tr(dy_rd + T::DY_PLANE + k1 * 64));
+      // patch pixel of tile pixel k at tap (0, 0)
+      const int p0 = (k0 / TC) * T::PC + k0 % TC, p1 = (k1 / TC) * T::PC + k1 % TC;
+      static_for<0, NT>([&](auto tc_) {
+        constexpr int tap = decltype(tc_)::value;
+        constexpr int toff = (KS == 3 ? (tap / 3) * T::PC + tap % 3 : 0) * 64;
+        const bf16x8 bhi = cat8(ds_read_tr(a_rd + p0 * 64 + toff), ds_read_tr(a_rd + p1 * 64 + toff));
+        if constexpr (MODE == MODE_F32X3) {
+          const bf16x8 blo = cat8(ds_read_tr(a_rd + T::A_PLANE + p0 * 64 + toff),
+                                  ds_read_tr(a_rd + T::A_PLANE + p1 * 64 + toff));
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[tap], 0, 0, 0);
+          acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[tap], 0, 0, 0);
+        }
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[tap], 0, 0, 0);
+      });
+    }
+  }
+  // partials: part[split][tap][Cout][Cin]; accumulator register r of lane l is
+  // row (co) (r & 3) + 8 (r >> 2) + 4 (l >> 5), column (ci) l & 31
+  static_for<0, NT>([&](auto tc_) {
+    constexpr int tap = decltype(tc_)::value;
+    float* dst = a.part + (((size_t)split * NT + tap) * Cout + co0 + wave * 32) * Cin + ci0 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * Cin] = acc[tap][r];
+  });
+#endif
+}
+
+// out[co][ci][tap] (+)= sum_s part[s][tap][co][ci], fixed order over s
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                                int S, int NT, int Cout, int Cin, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // co * Cin + ci
+  if (i >= Cout * Cin) return;
+  const size_t plane = (size_t)Cout * Cin;
+  for (int tap = 0; tap < NT; ++tap) {
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += part[((size_t)k * NT + tap) * plane + i];
+    float* o = out + (size_t)i * NT + tap;
+    *o = accumulate ? *o + s : s;
+  }
+}
+
+int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks) {
+  const int tc = ((W / d) % 64 == 0) ? 64 : 32;
+  const int total = B * (H / d) * (W / d) / 128 * d * d;
+  (void)tc;
+  const int blocks = (Cin / 32) * (Cout / 128);
+  int S = (512 + blocks - 1) / blocks;
+  S = S < total ? S : total;
+  return S < 1 ? 1 : S;
+}
+
+size_t wgrad_part_floats(int S, int Cin, int Cout, int ks) { return (size_t)S * ks * ks * Cin * Cout; }
+
+template <int MODE>
+static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
+  dim3 grid(S, a.Cin / 32, a.Cout / 128);
+  if (ks == 1) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 1>), grid, dim3(256), 0, st, a);
+  else if (tc == 64) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, int accumulate, hipStream_t st, const char** why) {
+  const int d = a.dil;
+  if (a.Cin % 32 || a.Cout % 128) { *why = "wgrad: Cin%32 and Cout%128 required"; return hipErrorInvalidValue; }
+  if (a.H % d || a.W % d) { *why = "wgrad: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
+  const int Ws = a.W / d, Hs = a.H / d;
+  const int tc = (Ws % 64 == 0) ? 64 : 32;
+  if (ks == 1 && (d != 1 || Ws % 64 || Hs % 2)) { *why = "wgrad: 1x1 needs d=1 and W%64"; return hipErrorInvalidValue; }
+  if (Ws % tc || Hs % (128 / tc)) { *why = "wgrad: sub-grid not divisible by the pixel tile"; return hipErrorInvalidValue; }
+  if (!a.circular && d != 1) { *why = "wgrad: zero padding only for d=1"; return hipErrorInvalidValue; }
+  if (!a.pro_ss) { *why = "wgrad: prologue table missing"; return hipErrorInvalidValue; }
+  const int S = wgrad_splits(a.B, a.H, a.W, d, a.Cin, a.Cout, ks);
+  if (!a.part || a.part_floats < wgrad_part_floats(S, a.Cin, a.Cout, ks)) {
+    *why = "wgrad: partial buffer too small";
+    return hipErrorInvalidValue;
+  }
+  hipError_t e;
+  switch (mode) {
+    case MODE_F32X3: e = wgrad_mode<MODE_F32X3>(a, ks, tc, S, st); break;
+    case MODE_BF16: e = wgrad_mode<MODE_BF16>(a, ks, tc, S, st); break;
+    default: *why = "wgrad: training runs in fp32x3 or bf16"; return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) return e;
+  const int n = a.Cout * a.Cin;
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a.part, out, S, ks * ks, a.Cout,
+                     a.Cin, accumulate);
+  return hipGetLastError();
+}
+
+}  // namespace sdp

@@ -44,6 +44,16 @@ _SIGS = {
     "sdp_net_destroy": (I, [P]),
     "sdp_net_profile_enable": (I, [P, I]),
     "sdp_net_profile_read": (I, [P, C.c_char_p, SZ, C.POINTER(I)]),
+    "sdp_net_param_arena_floats": (I, [P, C.POINTER(SZ)]),
+    "sdp_net_param_count": (I, [P, C.POINTER(I)]),
+    "sdp_net_param_info": (I, [P, I, C.c_char_p, SZ, C.POINTER(SZ), C.POINTER(SZ)]),
+    "sdp_net_bind_params": (I, [P, P, P]),
+    "sdp_net_repack": (I, [P, P]),
+    "sdp_net_train_workspace_size": (I, [P, I, C.POINTER(SZ)]),
+    "sdp_net_forward_train": (I, [P, P, P, P, I, P, SZ, P]),
+    "sdp_net_backward": (I, [P, P, I, P, SZ, P, P]),
+    "sdp_dsm_loss": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
+    "sdp_adam_ema_step": (I, [P, P, P, P, P, SZ, F, F, F, F, I, F, P]),
     "sdp_langevin_step": (I, [P, P, P, P, P, U64, U64, F, F, F, I, I, I, I, P, P, P]),
     "sdp_axpy_step": (I, [P, P, F, P, P, P, F, I, P]),
     "sdp_merge_workspace_size": (I, [I, I, I, I, C.POINTER(SZ)]),

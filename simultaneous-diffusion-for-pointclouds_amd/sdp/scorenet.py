@@ -51,6 +51,10 @@ class ScoreNet:
         self._ready = True
         return self
 
+    def param_shapes(self):
+        """(state_dict key, shape) of every learnable parameter (no 'sigmas' buffer)."""
+        return param_spec(self.ngf, self.channels).items()
+
     def load_synthetic(self):
         return self.load_state_dict(synthetic_state_dict(self.ngf, self.channels, self.num_classes))
 

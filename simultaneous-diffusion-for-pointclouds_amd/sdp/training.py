@@ -1,0 +1,200 @@
+"""DSM training of the score network on libsdp (BASELINE config 5).
+
+Mirrors the reference's training interface:
+  * ``anneal_dsm_score_estimation_with_mask`` -- LiDARGen/losses/dsm.py:67-119 (same
+    arguments; returns ``(loss, scores)``), computed by ``sdp_net_forward_train`` +
+    ``sdp_dsm_loss``;
+  * ``Trainer.backward()`` -- ``loss.backward()`` (runners/ncsn_runner_kitti_simultaneous.py:230)
+    through ``sdp_net_backward``;
+  * ``Trainer.step()`` -- ``optimizer.step()`` of ``get_optimizer`` (losses/__init__.py:10-20,
+    Adam) and ``EMAHelper.update`` (models/ema.py:16-21) in one fused kernel, then the packed
+    conv weights are rebuilt on the device;
+  * ``train_step`` -- one inner-loop iteration of the kitti runner's ``train()``
+    (runners/ncsn_runner_kitti_simultaneous.py:186-235).
+
+Data-parallel training: one process per GPU, gradients averaged with one RCCL all-reduce of
+the flat gradient arena (``dist_group``), the DDP equivalent of the reference's DataParallel.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .scorenet import ScoreNet
+
+
+class Trainer:
+    """Device-resident training state of one ScoreNet: parameter arena (bound to the net),
+    gradient arena, Adam moments and the EMA shadow, all in the net's parameter layout."""
+
+    def __init__(self, net: ScoreNet, lr: float = 1e-4, beta1: float = 0.9, beta2: float = 0.999,
+                 eps: float = 1e-8, ema: bool = True, ema_mu: float = 0.999, device="cuda", dist_group=None):
+        if net.precision not in ("fp32x3", "bf16"):
+            raise ValueError("training runs in precision fp32x3 or bf16")
+        L = _lib.lib()
+        self.net, self.L = net, L
+        self.lr, self.beta1, self.beta2, self.eps = lr, beta1, beta2, eps
+        self.ema, self.ema_mu = ema, ema_mu
+        self.dist_group = dist_group
+        n = _lib.SZ()
+        _lib.check(L.sdp_net_param_arena_floats(net._h, _lib.C.byref(n)), "param_arena_floats")
+        cnt = _lib.I()
+        _lib.check(L.sdp_net_param_count(net._h, _lib.C.byref(cnt)), "param_count")
+        self.layout = []
+        key = _lib.C.create_string_buffer(256)
+        off, numel = _lib.SZ(), _lib.SZ()
+        for i in range(cnt.value):
+            _lib.check(L.sdp_net_param_info(net._h, i, key, 256, _lib.C.byref(off), _lib.C.byref(numel)), "param_info")
+            self.layout.append((key.value.decode(), off.value, numel.value))
+        self.shapes = dict(net.param_shapes())
+        self.params = torch.empty(n.value, dtype=torch.float32, device=device)
+        _lib.check(L.sdp_net_bind_params(net._h, self.params.data_ptr(), _lib.stream()), "bind_params")
+        self.grads = torch.zeros_like(self.params)
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.shadow = self.params.clone() if ema else None       # EMAHelper.register (ema.py:10-14)
+        self.steps = 0
+        self._ws = {}
+        self._dscore = None
+        self._part = None
+        self._B = None
+
+    # ------------------------------------------------------------------ parameter views
+    def named_parameters(self, arena: torch.Tensor | None = None):
+        a = self.params if arena is None else arena
+        for k, off, numel in self.layout:
+            yield k, a[off:off + numel].view(self.shapes[k])
+
+    def named_grads(self):
+        return self.named_parameters(self.grads)
+
+    def state_dict(self):
+        return {k: v.detach().clone() for k, v in self.named_parameters()}
+
+    def ema_state_dict(self):
+        return {k: v.detach().clone() for k, v in self.named_parameters(self.shadow)}
+
+    # ------------------------------------------------------------------ forward / loss / backward
+    def _workspace(self, B):
+        ws = self._ws.get(B)
+        if ws is None:
+            n = _lib.SZ()
+            _lib.check(self.L.sdp_net_train_workspace_size(self.net._h, B, _lib.C.byref(n)), "train_workspace_size")
+            ws = torch.empty(n.value, dtype=torch.uint8, device=self.params.device)
+            self._ws[B] = ws
+        return ws
+
+    def forward(self, x: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+        """scores = scorenet(x, labels) in training mode (keeps the tape for backward)."""
+        net = self.net
+        if not x.is_cuda or x.dtype != torch.float32 or x.shape[1:] != (net.channels, net.H, net.W):
+            raise ValueError(f"Trainer.forward expects cuda float32 [B,{net.channels},{net.H},{net.W}]")
+        x = x.contiguous()
+        B = x.shape[0]
+        labels = labels.to(device=x.device, dtype=torch.int64).contiguous()
+        out = torch.empty_like(x)
+        ws = self._workspace(B)
+        _lib.check(self.L.sdp_net_forward_train(net._h, x.data_ptr(), labels.data_ptr(), out.data_ptr(), B,
+                                                ws.data_ptr(), ws.numel(), _lib.stream()), "forward_train")
+        self._B = B
+        return out
+
+    def dsm_loss(self, scores, used_sigmas, noise, masks, anneal_power=2.0):
+        """Masked DSM loss of losses/dsm.py:78-93; keeps d loss / d scores for backward()."""
+        B = scores.shape[0]
+        n_img = scores[0].numel()
+        sig = used_sigmas.reshape(B).to(device=scores.device, dtype=torch.float32).contiguous()
+        noise = noise.to(dtype=torch.float32).contiguous()
+        masks = masks.reshape(scores.shape).to(dtype=torch.float32).contiguous()
+        self._dscore = torch.empty_like(scores)
+        loss = torch.empty(1, dtype=torch.float32, device=scores.device)
+        per = torch.empty(B, dtype=torch.float32, device=scores.device)
+        if self._part is None or self._part.numel() < 2 * B * 64:
+            self._part = torch.empty(2 * B * 64, dtype=torch.float32, device=scores.device)
+        _lib.check(self.L.sdp_dsm_loss(scores.contiguous().data_ptr(), noise.data_ptr(), masks.data_ptr(),
+                                       sig.data_ptr(), B, n_img, float(anneal_power), self._dscore.data_ptr(),
+                                       loss.data_ptr(), per.data_ptr(), self._part.data_ptr(), _lib.stream()),
+                   "dsm_loss")
+        self.loss_per_sample = per
+        return loss.view(())
+
+    def zero_grad(self):
+        self.grads.zero_()
+
+    def backward(self, dscore: torch.Tensor | None = None):
+        """loss.backward(): gradient arena <- d loss / d parameters (averaged over ranks)."""
+        d = self._dscore if dscore is None else dscore.contiguous()
+        if d is None or self._B is None:
+            raise RuntimeError("Trainer.backward: run forward + dsm_loss first")
+        ws = self._workspace(self._B)
+        _lib.check(self.L.sdp_net_backward(self.net._h, d.data_ptr(), self._B, ws.data_ptr(), ws.numel(),
+                                           self.grads.data_ptr(), _lib.stream()), "backward")
+        if self.dist_group is not None:
+            import torch.distributed as dist
+            dist.all_reduce(self.grads, op=dist.ReduceOp.SUM, group=self.dist_group)
+            self.grads.div_(dist.get_world_size(self.dist_group))
+
+    def step(self):
+        """optimizer.step() (Adam) + ema_helper.update(score), then re-pack the conv weights."""
+        self.steps += 1
+        _lib.check(self.L.sdp_adam_ema_step(self.params.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
+                                            self.exp_avg_sq.data_ptr(),
+                                            self.shadow.data_ptr() if self.shadow is not None else None,
+                                            self.params.numel(), self.lr, self.beta1, self.beta2, self.eps,
+                                            self.steps, self.ema_mu, _lib.stream()), "adam_ema_step")
+        _lib.check(self.L.sdp_net_repack(self.net._h, _lib.stream()), "repack")
+
+
+def anneal_dsm_score_estimation_with_mask(scorenet: Trainer, perturbed_samples, used_sigmas, noise, masks, sky,
+                                          sigmas, labels=None, anneal_power=2., hook=None):
+    """losses/dsm.py:67-119 on libsdp.  ``scorenet`` is a Trainer; returns (loss, scores) and
+    leaves d loss / d scores in the trainer for ``scorenet.backward()`` (loss.backward())."""
+    B = perturbed_samples.shape[0]
+    if labels is None:
+        labels = torch.randint(0, len(sigmas), (B,), device=perturbed_samples.device)
+    if used_sigmas is None:
+        used_sigmas = sigmas[labels].view(B, *([1] * len(perturbed_samples.shape[1:])))
+        noise = torch.randn_like(perturbed_samples) * used_sigmas
+        perturbed_samples = perturbed_samples + noise
+    scores = scorenet.forward(perturbed_samples.float(), labels)
+    loss = scorenet.dsm_loss(scores, used_sigmas, noise, masks, anneal_power)
+    if hook is not None:
+        hook(scorenet.loss_per_sample, labels)
+    return loss, scores
+
+
+def get_optimizer(config, net: ScoreNet, **kw) -> Trainer:
+    """losses/__init__.py:10-20 (Adam only: the shipped configs' optimizer)."""
+    o = config.optim
+    if o.optimizer != "Adam":
+        raise NotImplementedError(f"optimizer {o.optimizer}: only Adam is built")
+    if getattr(o, "weight_decay", 0.0) or getattr(o, "amsgrad", False):
+        raise NotImplementedError("Adam with weight_decay / amsgrad is not built")
+    ema = bool(getattr(config.model, "ema", True))
+    return Trainer(net, lr=o.lr, beta1=o.beta1, beta2=0.999, eps=o.eps, ema=ema,
+                   ema_mu=getattr(config.model, "ema_rate", 0.999), **kw)
+
+
+def train_step(trainer: Trainer, X, originalX, mask, sigmas, timestep: int, step_lr: float, n_steps_each: int,
+               anneal_power: float = 2.0, generator=None):
+    """One timestep of the kitti runner's training loop (ncsn_runner_kitti_simultaneous.py:186-235):
+    noise the known pixels at sigma[timestep], DSM loss + backward + Adam + EMA, and advance X
+    by n_steps_each Langevin predictions of the unknown pixels.  Returns (loss, X_next)."""
+    B = X.shape[0]
+    labels = torch.full((B,), timestep, device=X.device, dtype=torch.int64)
+    sig = torch.as_tensor(sigmas, dtype=torch.float32, device=X.device)
+    used = sig[labels].view(B, 1, 1, 1)
+    noise = torch.randn(X.shape, device=X.device, generator=generator) * used
+    X = X + noise * mask
+    loss, grad = anneal_dsm_score_estimation_with_mask(trainer, X, used, noise, mask, None, sig, labels, anneal_power)
+    step_size = float(step_lr * (float(sig[timestep]) / float(sig[-1])) ** 2)
+    notm = torch.logical_not(mask).int()
+    for _ in range(n_steps_each):
+        noise2 = torch.randn(X.shape, device=X.device, generator=generator)
+        prediction = X + step_size * grad + noise2 * np.sqrt(step_size * 2)
+        X = originalX * mask + prediction * notm
+    trainer.zero_grad()
+    trainer.backward()
+    trainer.step()
+    return loss, X

@@ -170,3 +170,27 @@ def test_kitti_sampler_end_to_end(params128):
     np.testing.assert_allclose(images[0], f["new"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(images[1], f["new2"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(images[2], f["final"], rtol=1e-5, atol=1e-5)
+
+
+def dsm_case(H, W, B, tag="dsm"):
+    """Inputs of oracle/gen_golden.py gen_dsm (same generator stream)."""
+    r = GI.rng(tag)
+    X = torch.from_numpy(r.random((B, 2, H, W)).astype(np.float32))
+    noise = torch.from_numpy(r.standard_normal((B, 2, H, W)).astype(np.float32))
+    mask = torch.from_numpy((r.random((B, 2, H, W)) > 0.3).astype(np.float32))
+    labels = torch.tensor([3, 200][:B])
+    return X, noise, mask, labels
+
+
+def test_dsm_loss_and_gradients_oracle_matches_reference(params128):
+    """The oracle's autograd DSM loss/gradients reproduce the reference module's loss.backward()."""
+    f = _g("dsm_ngf128_b2_64x128.npz")
+    X, noise, mask, labels = dsm_case(64, 128, 2)
+    noise = noise * params128["sigmas"][labels].view(2, 1, 1, 1)
+    loss, scores, grads = R.dsm_loss_and_grads(params128, X + noise, noise, mask, labels)
+    assert abs(loss.item() - float(f["loss"])) <= 1e-5 * abs(float(f["loss"]))
+    assert np.abs(scores.numpy() - f["scores"]).max() <= 1e-6 * np.abs(f["scores"]).max()
+    keys = [str(k) for k in f["grad_keys"]]
+    assert set(keys) == set(grads)
+    for k, gn in zip(keys, f["grad_norms"]):
+        assert abs(grads[k].norm().item() - gn) <= 1e-4 * gn + 1e-6, k
