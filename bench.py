@@ -1,13 +1,20 @@
 """bench.py -- Langevin image-steps/s of the simultaneous sampler on MI355X (BASELINE.json metric).
 
-One step = one Langevin step of every view: score-net forward (libsdp) + fused update +
-cross-view consistency merge (a level >= minStepToShare, so the merge runs every step).
+Workloads (--workload):
+  line (default; BASELINE configs 2 and 4): one step = one Langevin step of every view:
+      score-net forward (libsdp) + fused update + cross-view consistency merge (a level >=
+      minStepToShare, so the merge runs every step), pose-matrix (kitti) merge, setting 5.
+  allforone (config 3): the same step with the origin-offset (AllForOne / Inpainting.yml)
+      merge, setting 7, target + 8 aux views = 9 views per GPU.
+  train (config 5): one DSM training step of the kitti runner (score-net forward, masked DSM
+      loss, backward, gradient all-reduce over RCCL, Adam + EMA, weight re-pack, 5 Langevin
+      predictions of the unknown pixels), batch 8 per GPU, bf16.  Prints its own metric.
 
-Modes (one process per GPU; torchrun sets RANK/LOCAL_RANK/WORLD_SIZE):
+Modes for line (one process per GPU; torchrun sets RANK/LOCAL_RANK/WORLD_SIZE):
   viewsplit (default): ONE megabatch of 4*N views (Line.yml 4 views on 1 GPU = config 2;
       32 views on 8 GPUs = config 4); each rank owns 4 views, all-gathers the megabatch's
       images over RCCL every step (the cross-view consistency gather) and merges into its own.
-  megabatch: every rank runs an independent 4-view megabatch (zero data exchange).
+  megabatch: every rank runs an independent megabatch (zero data exchange).
 Both: one 4-byte all_reduce(MAX) per step keeps the reference's global tooHigh exact.
 Per-GPU work is fixed as N grows ("scaling": "weak").  `value` = all views x steps / max-over-
 ranks wall time.  The dominant conv class is timed live with HIP events on the forward's
@@ -31,7 +38,12 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "Langevin denoising steps/sec on 64×1024 range images, 1/2/4/8 MI355X"
+TRAIN_METRIC = "DSM training image-steps/sec on 64×1024 range images (fwd+bwd+Adam+EMA), 1/2/4/8 MI355X"
 PEAK = {"fp32": 157.3, "fp32x3": 2500.0 / 3, "bf16": 2500.0}  # dense MFMA TFLOP/s in algorithmic fp32 FLOPs
+FWD_FLOP = 1.2663e12          # score-net forward FLOPs per 64x1024 image
+# Inpainting.yml (HDVMine_Circle.yml) data.modifications + 2 more origins: 8 aux views (config 3)
+CIRCLE9 = [[0, 0, 0], [5, -5, 0], [-5, -5, 0], [0, 5, 0], [-10, 10, 0], [10, 10, 0], [-10, 0, 0], [10, 0, 0],
+           [0, -10, 0]]
 
 
 def parse():
@@ -39,15 +51,24 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--views", type=int, default=4, help="views per GPU")
+    ap.add_argument("--workload", choices=["line", "allforone", "train"], default="line")
+    ap.add_argument("--views", type=int, default=None, help="views (or training images) per GPU")
     ap.add_argument("--mode", choices=["viewsplit", "megabatch"], default="viewsplit")
-    ap.add_argument("--precision", choices=["fp32x3", "fp32", "bf16"], default="fp32x3")
+    ap.add_argument("--precision", choices=["fp32x3", "fp32", "bf16"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.views is None:
+        a.views = {"line": 4, "allforone": 9, "train": 8}[a.workload]
+    if a.precision is None:
+        a.precision = "bf16" if a.workload == "train" else "fp32x3"
+    if a.workload == "allforone":
+        a.mode = "megabatch"
+    return a
 
 
-def cpu_baseline(V, H, W, threads):
+# ----------------------------------------------------------------------------- CPU baselines
+def cpu_baseline(V, H, W, threads, workload):
     """Oracle restatement (torch-CPU score net + numpy update + numpy merge), one step of V views."""
     from oracle import sampling_ref as S
     from oracle import scorenet_ref as R
@@ -67,11 +88,32 @@ def cpu_baseline(V, H, W, threads):
     s = S.step_size_of(6.2e-6, sig[c], sig[-1])
     x1, _ = S.langevin_update(x.numpy(), S.nan_to_num(grad), sc["ref"], sc["mask"],
                               np.random.default_rng(0).standard_normal(x.shape).astype(np.float32), s, 1.0)
-    S.kitti_merge(x1, sc["mask"], sc["sky"], ex, sc["toWorld"], sc["fromWorld"], V, sig[c])
+    if workload == "allforone":
+        S.allforone_merge(x1, sc["mask"], sc["sky"], ex, np.asarray(CIRCLE9[:V]), V, sig[c])
+    else:
+        S.kitti_merge(x1, sc["mask"], sc["sky"], ex, sc["toWorld"], sc["fromWorld"], V, sig[c])
     dt = time.perf_counter() - t0
     return {"value": V / dt, "unit": "image-steps/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"1 Langevin step of {V} views at {H}x{W} (fwd + update + merge), oracle restatement "
-                      f"(torch CPU fp32 + numpy), {dt:.2f} s"}
+            "sample": f"1 Langevin step of {V} views at {H}x{W} (fwd + update + {workload} merge), oracle "
+                      f"restatement (torch CPU fp32 + numpy), {dt:.2f} s"}
+
+
+def cpu_baseline_train(H, W, threads):
+    """Oracle autograd DSM step (fwd + loss + backward) of ONE image, torch CPU fp32."""
+    from oracle import scorenet_ref as R
+    from sdp.weights import synthetic_state_dict
+    torch.set_num_threads(max(1, min(threads, os.cpu_count() or 1)))
+    P = R.to_torch_params(synthetic_state_dict(128))
+    g = torch.Generator().manual_seed(1234)
+    X = torch.rand(1, 2, H, W, generator=g)
+    noise = torch.randn(1, 2, H, W, generator=g) * 50
+    mask = (torch.rand(1, 2, H, W, generator=g) > 0.25).float()
+    t0 = time.perf_counter()
+    R.dsm_loss_and_grads(P, X + noise, noise, mask, torch.tensor([0]))
+    dt = time.perf_counter() - t0
+    return {"value": 1 / dt, "unit": "image-steps/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"1 DSM step (fwd + loss + backward, no optimizer) of 1 image at {H}x{W}, oracle autograd "
+                      f"(torch CPU fp32), {dt:.2f} s"}
 
 
 def pmc_traffic(precision, V):
@@ -92,24 +134,36 @@ def pmc_traffic(precision, V):
     return None
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+# ----------------------------------------------------------------------------- timing harness
+def timed(step, args, dist, dev):
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
     if dist:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = t.item()
+    return dt
+
+
+def run_sampling(args, rank, N, dist, dev):
     from sdp import _lib
-    from sdp.merge import Merger
+    from sdp.merge import Merger, allforone_origins
     from sdp.scorenet import ScoreNet
     from sdp.synthetic import exist_mask, scene_views
     from sdp.weights import get_sigmas_np
 
     H, W, V = 64, 1024, args.views
-    N = world
     if args.mode == "viewsplit":
         n_src, aB, o_begin = V * N, V * N, rank * V
         sc = scene_views(n_src, H, W)
@@ -122,9 +176,18 @@ def main():
     x = x_all[o_begin:o_begin + V]                      # own views: a contiguous slice of the megabatch
     ref = torch.from_numpy(sc["ref"][o_begin:o_begin + V]).to(dev)
     mask = torch.from_numpy(sc["mask"][o_begin:o_begin + V]).to(dev)
-    merger = Merger(n_src, aB, H, W, dev, torch.from_numpy(exist_mask(H, W)), torch.from_numpy(sc["sky"]),
-                    torch.from_numpy(sc["mask"]), toWorld=torch.from_numpy(sc["toWorld"]),
-                    fromWorld=torch.from_numpy(sc["fromWorld"]), o_begin=o_begin, n_out=V)
+    if args.workload == "allforone":
+        if V > len(CIRCLE9):
+            raise SystemExit(f"allforone: at most {len(CIRCLE9)} views")
+        merger = Merger(n_src, aB, H, W, dev, torch.from_numpy(exist_mask(H, W)), torch.from_numpy(sc["sky"]),
+                        torch.from_numpy(sc["mask"]), origins=allforone_origins(CIRCLE9[:V]), o_begin=o_begin,
+                        n_out=V)
+        setting = 7
+    else:
+        merger = Merger(n_src, aB, H, W, dev, torch.from_numpy(exist_mask(H, W)), torch.from_numpy(sc["sky"]),
+                        torch.from_numpy(sc["mask"]), toWorld=torch.from_numpy(sc["toWorld"]),
+                        fromWorld=torch.from_numpy(sc["fromWorld"]), o_begin=o_begin, n_out=V)
+        setting = 5
     sig = get_sigmas_np()
     lik = torch.empty_like(x)
     absmax = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -148,56 +211,115 @@ def main():
             if args.mode == "viewsplit":
                 torch.distributed.all_gather_into_tensor(x_all, x)     # cross-view consistency gather
             torch.distributed.all_reduce(absmax, op=torch.distributed.ReduceOp.MAX)
-        merger(x_all, sig[c], 5, 10, 0.01, absmax)
+        merger(x_all, sig[c], setting, 10, 0.01, absmax)
 
+    net.profile(True)
+    net.profile_read()
     for i in range(args.warmup):
         step(i)
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    net.profile(True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    if dist:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t0
+    net.profile_read()                                  # drop the warmup launches
+    dt = timed(step, argparse.Namespace(warmup=0, steps=args.steps), dist, dev)
     prof = net.profile_read()
     net.profile(False)
-    if dist:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = t.item()
     assert torch.isfinite(x_all).all(), "non-finite images"
-    if rank == 0:
-        for k, (n_, ms_, fl_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
-            print(f"[conv] {k:34s} launches {n_:5d} avg {ms_ / n_ * 1e3:8.1f} us  {fl_ / (ms_ / n_ / 1e3) / 1e12:7.1f} TF/s",
-                  file=sys.stderr)
-        value = N * V * args.steps / dt
-        cls, (n, ms, fl) = max(prof.items(), key=lambda kv: kv[1][1])
-        avg_s = ms / n / 1e3
-        achieved = fl / avg_s / 1e12
-        conv_ms = sum(v[1] for v in prof.values()) / args.steps
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[args.precision], 1),
-                "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4),
-                "traffic": pmc_traffic(args.precision, V), "traffic_unit": "bytes/launch (PMC, profiles/r01_traffic.json)",
-                "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if args.precision == "bf16" else 4),
-                "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
-                "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3)}
-        cpu = None
-        if N == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(V, H, W, args.cpu_threads)
-        line = {"metric": METRIC, "value": round(value, 3), "unit": "image-steps/s", "n_gpus": N,
-                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-                "data": "synthetic (procedural Line.yml-style scene, random-init NCSN_LiDAR_small weights)",
-                "config": {"workload": "Line.yml simultaneous sampling step (score-net fwd + Langevin update + "
-                                       "consistency merge), 64x1024x2 range images",
-                           "views_per_gpu": V, "megabatch_views": aB, "mode": args.mode,
-                           "conv_arithmetic": args.precision, "parallelism": f"views{N}"},
-                "roofline": roof, "cpu_baseline": cpu}
+    if rank != 0:
+        return None
+    for k, (n_, ms_, fl_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+        print(f"[conv] {k:34s} launches {n_:5d} avg {ms_ / n_ * 1e3:8.1f} us  {fl_ / (ms_ / n_ / 1e3) / 1e12:7.1f} TF/s",
+              file=sys.stderr)
+    value = N * V * args.steps / dt
+    cls, (n, ms, fl) = max(prof.items(), key=lambda kv: kv[1][1])
+    avg_s = ms / n / 1e3
+    achieved = fl / avg_s / 1e12
+    conv_ms = sum(v[1] for v in prof.values()) / args.steps
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[args.precision], 1),
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4),
+            "traffic": pmc_traffic(args.precision, V) if args.workload == "line" else None,
+            "traffic_unit": "bytes/launch (PMC, profiles/r01_traffic.json)",
+            "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if args.precision == "bf16" else 4),
+            "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
+            "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3)}
+    cpu = None
+    if N == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(V, H, W, args.cpu_threads, args.workload)
+    if args.workload == "allforone":
+        wl = ("Inpainting.yml AllForOne simultaneous sampling step (score-net fwd + Langevin update + origin-offset "
+              "consistency merge, setting 7), target + 8 aux views, 64x1024x2 range images")
+    else:
+        wl = ("Line.yml simultaneous sampling step (score-net fwd + Langevin update + consistency merge), "
+              "64x1024x2 range images")
+    return {"metric": METRIC, "value": round(value, 3), "unit": "image-steps/s", "n_gpus": N,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (procedural Line.yml-style scene, random-init NCSN_LiDAR_small weights)",
+            "config": {"workload": wl, "views_per_gpu": V, "megabatch_views": aB, "mode": args.mode,
+                       "conv_arithmetic": args.precision, "parallelism": f"views{N}"},
+            "roofline": roof, "cpu_baseline": cpu}
+
+
+def run_train(args, rank, N, dist, dev):
+    from sdp.scorenet import ScoreNet
+    from sdp.synthetic import scene_views
+    from sdp.training import Trainer, train_step
+    from sdp.weights import get_sigmas_np
+
+    H, W, Bg = 64, 1024, args.views
+    net = ScoreNet(H=H, W=W, precision=args.precision).load_synthetic()
+    tr = Trainer(net, lr=1e-4, dist_group=torch.distributed.group.WORLD if dist else None)
+    sc = scene_views(Bg, H, W, seed=1234 + rank)
+    X0 = torch.from_numpy(sc["ref"]).to(dev)
+    mask = torch.from_numpy(sc["mask"]).to(dev).float()
+    sig = get_sigmas_np()
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    state = {"X": X0.clone(), "t": 0}
+    losses = []
+
+    def step(i):
+        t = i % 4                    # the runner's curriculum: timesteps 0 .. maxTimeStepReachable-1
+        loss, state["X"] = train_step(tr, state["X"], X0, mask, sig, t, 6.2e-6, 5, generator=gen)
+        losses.append(loss)
+
+    dt = timed(step, args, dist, dev)
+    if not all(np.isfinite(float(v)) for v in losses):
+        raise SystemExit("non-finite training loss")
+    if rank != 0:
+        return None
+    value = N * Bg * args.steps / dt
+    ms = dt / args.steps * 1e3
+    flops = 3 * FWD_FLOP * Bg                          # fwd + dgrad + wgrad conv FLOPs per GPU-step
+    achieved = flops / (ms / 1e3) / 1e12
+    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[args.precision], 1),
+            "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4), "traffic": None,
+            "kernel": "whole training step (conv fwd + dgrad + wgrad FLOPs / step time)"}
+    cpu = None
+    if N == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_train(H, W, args.cpu_threads)
+    return {"metric": TRAIN_METRIC, "value": round(value, 3), "unit": "image-steps/s", "n_gpus": N,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "synthetic (procedural scene range images, random-init NCSN_LiDAR_small weights)",
+            "config": {"workload": "Densification.yml DSM training step (kitti runner loop body: fwd + masked DSM "
+                                   "loss + backward + grad all-reduce + Adam + EMA + 5 Langevin predictions)",
+                       "batch_per_gpu": Bg, "global_batch": Bg * N, "parallelism": f"dp{N}",
+                       "conv_arithmetic": args.precision},
+            "roofline": roof, "cpu_baseline": cpu, "final_loss": float(losses[-1])}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+    if args.workload == "train":
+        line = run_train(args, rank, world, dist, dev)
+    else:
+        line = run_sampling(args, rank, world, dist, dev)
+    if line is not None:
         print(json.dumps(line))
     if dist:
         torch.distributed.destroy_process_group()
