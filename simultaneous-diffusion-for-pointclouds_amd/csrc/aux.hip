@@ -198,8 +198,10 @@ __global__ __launch_bounds__(1024) void inpp_finalize_kernel(const float2* __res
 }
 
 // ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
+// idx (training): window position 0..24 of the max in row-major window order, the first one
+// on ties -- the index torch's max_pool2d keeps for its backward
 __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                       int B, int H, int W, int C) {
+                                                       uchar4* __restrict__ idx, int B, int H, int W, int C) {
   const int C4 = C / 4;
   const size_t n = (size_t)B * H * W * C4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -210,6 +212,7 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
     const int y = p % H;
     const int b = p / H;
     float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    uchar4 bi = make_uchar4(12, 12, 12, 12);
     for (int dy = -2; dy <= 2; ++dy) {
       const int yy = y + dy;
       if (yy < 0 || yy >= H) continue;
@@ -217,10 +220,15 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
         const int xx = x + dx;
         if (xx < 0 || xx >= W) continue;
         const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
-        m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+        const unsigned char k = (unsigned char)((dy + 2) * 5 + dx + 2);
+        if (v.x > m.x) { m.x = v.x; bi.x = k; }
+        if (v.y > m.y) { m.y = v.y; bi.y = k; }
+        if (v.z > m.z) { m.z = v.z; bi.z = k; }
+        if (v.w > m.w) { m.w = v.w; bi.w = k; }
       }
     }
     *reinterpret_cast<float4*>(out + i * 4) = m;
+    if (idx) idx[i] = bi;
   }
 }
 
@@ -245,10 +253,10 @@ hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, con
   return hipGetLastError();
 }
 
-hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st) {
+hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
   const size_t n = (size_t)B * H * W * (C / 4);
   const int grid = (int)std::min<size_t>((n + 255) / 256, 256 * 16);
-  hipLaunchKernelGGL(maxpool5_kernel, dim3(grid), dim3(256), 0, st, in, out, B, H, W, C);
+  hipLaunchKernelGGL(maxpool5_kernel, dim3(grid), dim3(256), 0, st, in, out, reinterpret_cast<uchar4*>(idx), B, H, W, C);
   return hipGetLastError();
 }
 

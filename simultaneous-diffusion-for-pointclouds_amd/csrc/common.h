@@ -73,6 +73,7 @@ struct WgradArgs {
   const float* dy;         // gradient of the conv output (before any pooling) [B][H][W][Cout]
   float* part;             // split partials [S][k*k][Cout][Cin]
   size_t part_floats;
+  float* bpart;            // bias-gradient partials [S][Cout] (S <= 1024) or null
   int B, H, W, Cin, Cout, dil, circular;
 };
 

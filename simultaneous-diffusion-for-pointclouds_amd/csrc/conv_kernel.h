@@ -321,7 +321,6 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
       auto dmas = [&]() __attribute__((always_inline)) {
         if constexpr (tap == NT - 1) load_ss(min(chunk + 2, nchunks - 1));
         static_for<0, NU>([&](auto kc) {
-          constexpr int k = decltype(kc)::value;
           constexpr int dt = NT > XT ? XT : 0;   // all at the first free tap: the longest flight
           if constexpr (dt == tap) load_unit(kc, chunk + 2);
         });

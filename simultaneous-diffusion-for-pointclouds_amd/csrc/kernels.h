@@ -11,7 +11,7 @@ hipError_t end_conv(const float* in, const float* ss, const float* w, const floa
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st);
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
                          const float* beta, float* ss, hipStream_t st, float* nst = nullptr);
-hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st);
+hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx = nullptr);
 hipError_t langevin_step(float* x, const float* g, const float* ref, const int32_t* mask, const float* noise,
                          uint64_t seed, uint64_t offset, float step, float nscale, float gref, int n2n, int B, int C,
                          int HW, float* lik_out, uint32_t* absmax, hipStream_t st);
@@ -21,12 +21,11 @@ hipError_t axpy_step(float* x, const float* g, float a, const float* lik, const 
 // ---- training (DSM backward; train_aux.hip, wgrad.hip, conv_bwd.hip)
 hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k, int mode, int dgrad, hipStream_t st);
 hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
-                         int HW, int C, float* part, float* coef, float* dalpha, float* dgamma, float* dbeta,
-                         const float* r1, const float* r2, float* out, hipStream_t st);
-hipError_t chan_sum(const float* dy, size_t npix, int C, float* part, float* out, hipStream_t st);
+                         int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
+                         float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st);
 hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hipStream_t st);
-hipError_t maxpool5_backward(const float* src, const float* dp, const float* res, float* dst, uint8_t* idx, int B, int H,
-                             int W, int C, hipStream_t st);
+hipError_t maxpool5_backward(const uint8_t* idx, const float* dp, const float* res, float* dst, int B, int H, int W, int C,
+                             hipStream_t st);
 hipError_t upsample_backward(const float* g, float* dlow, int B, int H, int W, int C, int accumulate, hipStream_t st);
 hipError_t elu_backward_post(const float* dy, const float* y, const float* res, float* dst, size_t n, hipStream_t st);
 hipError_t add_tensors(const float* a, const float* b, float* dst, size_t n, hipStream_t st);
@@ -42,6 +41,7 @@ hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow,
 hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char** why);
 int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks);
 size_t wgrad_part_floats(int S, int Cin, int Cout, int ks);
-hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, int accumulate, hipStream_t st, const char** why);
+hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,
+                      const char** why);
 
 }  // namespace sdp

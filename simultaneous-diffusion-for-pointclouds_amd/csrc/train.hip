@@ -36,12 +36,12 @@ struct TrainPlan {
   size_t cap = 0, used = 0;
   std::map<std::string, T4> saved;
   std::map<std::string, float*> fl;   // saved per-norm tables: "<key>#ss", "<key>#nst"
+  std::map<std::string, uint8_t*> idxs;  // saved maxpool argmax indices
   float* stats = nullptr;
   float* xin = nullptr;               // copy of the forward input [B,2,H,W]
   int64_t* lab = nullptr;             // copy of the labels
   // backward scratch
-  float *wpart = nullptr, *spart = nullptr, *coef = nullptr, *cpart = nullptr, *epart = nullptr;
-  uint8_t* idx = nullptr;
+  float *wpart = nullptr, *bpart = nullptr, *spart = nullptr, *coef = nullptr, *ppart = nullptr, *epart = nullptr;
   size_t wpart_n = 0;
   float* grads = nullptr;
   size_t fwd_bytes = 0;
@@ -203,13 +203,18 @@ struct TrainPlan {
   T4 crpf(const std::string& k, const T4& X) {
     saved[k + ".X"] = X;
     T4 p1 = like(X), path1 = like(X), x1 = like(X), p2 = like(X), x2 = like(X);
-    if (!dry) ok(maxpool5(X.p, p1.p, B, X.H, X.W, X.C, st), "maxpool5");
+    const size_t nidx = (n(X) + 3) / 4;                // argmax bytes, in floats
+    uint8_t* i1 = reinterpret_cast<uint8_t*>(take(nidx));
+    uint8_t* i2 = reinterpret_cast<uint8_t*>(take(nidx));
+    idxs[k + ".i1"] = i1;
+    idxs[k + ".i2"] = i2;
+    if (!dry) ok(maxpool5(X.p, p1.p, B, X.H, X.W, X.C, st, i1), "maxpool5");
     Opt a;
     a.bias = false;
     a.out2 = x1.p;
     a.res2 = X.p;
     conv(p1, k + ".convs.0", path1, a);
-    if (!dry) ok(maxpool5(path1.p, p2.p, B, X.H, X.W, X.C, st), "maxpool5");
+    if (!dry) ok(maxpool5(path1.p, p2.p, B, X.H, X.W, X.C, st, i2), "maxpool5");
     Opt b;
     b.bias = false;
     b.res = x1.p;
@@ -254,6 +259,7 @@ struct TrainPlan {
     used = 0;
     saved.clear();
     fl.clear();
+    idxs.clear();
     xin = take((size_t)B * 2 * H * W);
     lab = reinterpret_cast<int64_t*>(take((size_t)B * 2));
     if (!dry) {
@@ -285,7 +291,8 @@ struct TrainPlan {
   }
 
   // ------------------------------------------------------------------ backward pieces
-  void wgrad(const std::string& k, const T4& in, int pro, const float* ss, const T4& dy, int dil, bool circular, int ks) {
+  void wgrad(const std::string& k, const T4& in, int pro, const float* ss, const T4& dy, int dil, bool circular, int ks,
+             bool with_bias) {
     if (dry) return;
     WgradArgs a{};
     a.in = in.p;
@@ -295,6 +302,7 @@ struct TrainPlan {
     a.dy = dy.p;
     a.part = wpart;
     a.part_floats = wpart_n;
+    a.bpart = bpart;
     a.B = B;
     a.H = in.H;
     a.W = in.W;
@@ -303,7 +311,8 @@ struct TrainPlan {
     a.dil = dil;
     a.circular = circular ? 1 : 0;
     const char* why = "wgrad launch";
-    ok(conv_wgrad(net->mode, a, ks, G(k + ".weight"), 0, st, &why), std::string(why) + " (" + k + ")");
+    ok(conv_wgrad(net->mode, a, ks, G(k + ".weight"), with_bias ? G(k + ".bias") : nullptr, 0, st, &why),
+       std::string(why) + " (" + k + ")");
   }
   void dgrad(const std::string& k, const T4& dy, const T4& dx, int dil, bool circular, int ks, int dact,
              const float* aux, const float* epi_ss, const float* res) {
@@ -328,14 +337,10 @@ struct TrainPlan {
     const char* why = "dgrad launch";
     ok(conv_dgrad(net->mode, a, ks, st, &why), std::string(why) + " (" + k + ")");
   }
-  void bias(const std::string& k, const T4& dy) {
-    if (dry) return;
-    ok(chan_sum(dy.p, (size_t)B * dy.H * dy.W, dy.C, cpart, G(k + ".bias"), st), "chan_sum " + k);
-  }
   void inpp_back(const std::string& nkey, const T4& g, const T4& h, const float* r1, const float* r2, const T4& out) {
     if (dry) return;
     ok(inpp_backward(g.p, h.p, F(nkey + "#nst"), P(nkey + ".alpha"), P(nkey + ".gamma"), B, h.H * h.W, h.C, spart, coef,
-                     G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st),
+                     ppart, G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st),
        "inpp_backward " + nkey);
   }
 
@@ -347,21 +352,17 @@ struct TrainPlan {
     if (down && dil == 1) {
       T4 dyf = mk(x.H, x.W, dout.C);
       if (!dry) ok(unpool(dout.p, dyf.p, B, x.H, x.W, dout.C, st), "unpool");
-      wgrad(k + ".conv2.conv", h1, PRO_AFFINE_ELU, ss2, dyf, 1, false, 3);
-      bias(k + ".conv2.conv", dyf);
+      wgrad(k + ".conv2.conv", h1, PRO_AFFINE_ELU, ss2, dyf, 1, false, 3, true);
       dgrad(k + ".conv2.conv", dyf, g2, 1, false, 3, 3, h1.p, ss2, nullptr);
-      wgrad(k + ".shortcut.conv", x, PRO_NONE, nullptr, dyf, 1, false, 1);
-      bias(k + ".shortcut.conv", dyf);
+      wgrad(k + ".shortcut.conv", x, PRO_NONE, nullptr, dyf, 1, false, 1, true);
       T4 sgb = like(x);
       dgrad(k + ".shortcut.conv", dyf, sgb, 1, false, 1, 0, nullptr, nullptr, nullptr);
       sg = sgb.p;
     } else {
-      wgrad(k + ".conv2", h1, PRO_AFFINE_ELU, ss2, dout, dil, true, 3);
-      bias(k + ".conv2", dout);
+      wgrad(k + ".conv2", h1, PRO_AFFINE_ELU, ss2, dout, dil, true, 3, true);
       dgrad(k + ".conv2", dout, g2, dil, true, 3, 3, h1.p, ss2, nullptr);
       if (down) {
-        wgrad(k + ".shortcut", x, PRO_NONE, nullptr, dout, dil, true, 3);
-        bias(k + ".shortcut", dout);
+        wgrad(k + ".shortcut", x, PRO_NONE, nullptr, dout, dil, true, 3, true);
         T4 sgb = like(x);
         dgrad(k + ".shortcut", dout, sgb, dil, true, 3, 0, nullptr, nullptr, nullptr);
         sg = sgb.p;
@@ -371,8 +372,7 @@ struct TrainPlan {
     }
     T4 dh1 = like(h1);
     inpp_back(k + ".normalize2", g2, h1, nullptr, nullptr, dh1);
-    wgrad(k + ".conv1", x, PRO_AFFINE_ELU, ss1, dh1, dil, true, 3);
-    bias(k + ".conv1", dh1);
+    wgrad(k + ".conv1", x, PRO_AFFINE_ELU, ss1, dh1, dil, true, 3, true);
     T4 g1 = like(x);
     dgrad(k + ".conv1", dh1, g1, dil, true, 3, 3, x.p, ss1, nullptr);
     T4 dx = like(x);
@@ -389,10 +389,10 @@ struct TrainPlan {
     for (int i = nb - 1; i >= 0; --i) {
       const std::string c1 = k + "." + std::to_string(i + 1) + "_1_conv", c2 = k + "." + std::to_string(i + 1) + "_2_conv";
       const T4 &xi = S(k + ".x" + std::to_string(i)), &ti = S(k + ".t" + std::to_string(i));
-      wgrad(c2, ti, PRO_ELU, nullptr, d, 1, true, 3);
+      wgrad(c2, ti, PRO_ELU, nullptr, d, 1, true, 3, false);
       T4 dt = like(ti);
       dgrad(c2, d, dt, 1, true, 3, 1, ti.p, nullptr, nullptr);
-      wgrad(c1, xi, PRO_ELU, nullptr, dt, 1, true, 3);
+      wgrad(c1, xi, PRO_ELU, nullptr, dt, 1, true, 3, false);
       T4 dn = like(xi);
       dgrad(c1, dt, dn, 1, true, 3, 1, xi.p, nullptr, d.p);
       d = dn;
@@ -400,17 +400,17 @@ struct TrainPlan {
     return d;
   }
   T4 crpb(const std::string& k, const T4& dx2) {
-    const T4 &X = S(k + ".X"), &p1 = S(k + ".p1"), &path1 = S(k + ".path1"), &p2 = S(k + ".p2");
-    wgrad(k + ".convs.1", p2, PRO_NONE, nullptr, dx2, 1, true, 3);
+    const T4 &X = S(k + ".X"), &p1 = S(k + ".p1"), &p2 = S(k + ".p2");
+    wgrad(k + ".convs.1", p2, PRO_NONE, nullptr, dx2, 1, true, 3, false);
     T4 dp2 = like(X);
     dgrad(k + ".convs.1", dx2, dp2, 1, true, 3, 0, nullptr, nullptr, nullptr);
     T4 dpath1 = like(X);
-    if (!dry) ok(maxpool5_backward(path1.p, dp2.p, dx2.p, dpath1.p, idx, B, X.H, X.W, X.C, st), "maxpool5_backward");
-    wgrad(k + ".convs.0", p1, PRO_NONE, nullptr, dpath1, 1, true, 3);
+    if (!dry) ok(maxpool5_backward(idxs.at(k + ".i2"), dp2.p, dx2.p, dpath1.p, B, X.H, X.W, X.C, st), "maxpool5_backward");
+    wgrad(k + ".convs.0", p1, PRO_NONE, nullptr, dpath1, 1, true, 3, false);
     T4 dp1 = like(X);
     dgrad(k + ".convs.0", dpath1, dp1, 1, true, 3, 0, nullptr, nullptr, nullptr);
     T4 dX = like(X);
-    if (!dry) ok(maxpool5_backward(X.p, dp1.p, dx2.p, dX.p, idx, B, X.H, X.W, X.C, st), "maxpool5_backward");
+    if (!dry) ok(maxpool5_backward(idxs.at(k + ".i1"), dp1.p, dx2.p, dX.p, B, X.H, X.W, X.C, st), "maxpool5_backward");
     return dX;
   }
   // returns the gradients of the refine block's inputs (second one empty for refine1)
@@ -426,12 +426,10 @@ struct TrainPlan {
       dm1 = mk(hB.H, hB.W, X.C);
       if (!dry) ok(upsample_backward(dm.p, dm1.p, B, X.H, X.W, X.C, 0, st), "upsample_backward");
     }
-    wgrad(k + ".msf.convs.0", hA, PRO_NONE, nullptr, dm, 1, true, 3);
-    bias(k + ".msf.convs.0", dm);
+    wgrad(k + ".msf.convs.0", hA, PRO_NONE, nullptr, dm, 1, true, 3, true);
     T4 dhA = like(hA);
     dgrad(k + ".msf.convs.0", dm, dhA, 1, true, 3, 0, nullptr, nullptr, nullptr);
-    wgrad(k + ".msf.convs.1", hB, PRO_NONE, nullptr, dm1, 1, true, 3);
-    bias(k + ".msf.convs.1", dm1);
+    wgrad(k + ".msf.convs.1", hB, PRO_NONE, nullptr, dm1, 1, true, 3, true);
     T4 dhB = like(hB);
     dgrad(k + ".msf.convs.1", dm1, dhB, 1, true, 3, 0, nullptr, nullptr, nullptr);
     return {rcub(k + ".adapt_convs.0", dhA, 2, false), rcub(k + ".adapt_convs.1", dhB, 2, false)};
@@ -445,9 +443,9 @@ struct TrainPlan {
     wpart = take(wpart_n);
     spart = take((size_t)B * (H * W / 512) * 256 * 2);
     coef = take((size_t)B * 256 * 4);
-    cpart = take(256 * 256);
-    epart = take(std::max((size_t)B * (H / 8) * (W / 32) * (2 * 128 * 9 + 2), (size_t)B * (H / 8) * (W / 64) * 128 * 37));
-    idx = reinterpret_cast<uint8_t*>(take((size_t)B * H * W * C / 4));
+    bpart = take(1024 * 256);
+    ppart = take((size_t)B * 256 * 3);
+    epart = take(std::max((size_t)B * (H / 32) * (W / 32) * (2 * 128 * 9 + 2), (size_t)B * (H / 32) * (W / 64) * 128 * 37));
     if (!dry) ok(hipMemsetAsync(grads, 0, net->arena_floats * 4, st), "zero grads");
 
     // head: IN++ -> ELU -> end_conv -> / sigma

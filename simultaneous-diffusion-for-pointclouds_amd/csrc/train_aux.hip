@@ -6,10 +6,9 @@
 //                    per-(b,c) coefficients dh = k1*g + k2*h + k3 and the alpha/gamma/beta
 //                    gradients -> the apply pass
 //   unpool         : adjoint of ConvMeanPool's 2x2 mean (layers.py:309-313)
-//   maxpool5 bwd   : adjoint of MaxPool2d(5, 1, 2) (layers.py:70), first-max tie rule
+//   maxpool5 bwd   : adjoint of MaxPool2d(5, 1, 2) (layers.py:70) from the forward's argmax indices
 //   upsample bwd   : adjoint of F.interpolate(bilinear, align_corners=True) (layers.py:182)
 //   elu bwd        : dy * elu'(from the ELU output)
-//   chan_sum       : bias gradients
 //   begin/end conv : weight gradients of the 4->128 / 128->2 convs, data gradient of end_conv
 //   dsm loss       : anneal_dsm_score_estimation_with_mask (losses/dsm.py:67-119) + d loss/d score
 //   adam_ema       : torch.optim.Adam step (losses/__init__.py:10-20) + EMAHelper.update (ema.py:16-21)
@@ -123,70 +122,73 @@ __global__ __launch_bounds__(256) void inpp_bwd_reduce_kernel(const float* __res
 __global__ __launch_bounds__(1024) void inpp_bwd_finalize_kernel(const float2* __restrict__ part, int ngrp, float N,
                                                                  const float4* __restrict__ nst,
                                                                  const float* __restrict__ alpha,
-                                                                 const float* __restrict__ gamma, int B, int C,
-                                                                 float4* __restrict__ coef, float* __restrict__ dalpha,
-                                                                 float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                                 const float* __restrict__ gamma, int C,
+                                                                 float4* __restrict__ coef, float* __restrict__ ppart) {
   __shared__ double r0[1024], r1[1024];
-  const int tid = threadIdx.x, Gt = 1024 / C, gi = tid / C, c = tid % C;
-  double acc_a = 0.0, acc_g = 0.0, acc_b = 0.0;
+  const int b = blockIdx.x, tid = threadIdx.x, Gt = 1024 / C, gi = tid / C, c = tid % C;
+  double s0 = 0.0, s1 = 0.0;
+  for (int k = gi; k < ngrp; k += Gt) {
+    const float2 v = part[((size_t)b * ngrp + k) * C + c];
+    s0 += v.x;
+    s1 += v.y;
+  }
+  r0[tid] = s0;
+  r1[tid] = s1;
+  __syncthreads();
+  if (gi == 0)
+    for (int k = 1; k < Gt; ++k) {
+      s0 += r0[k * C + c];
+      s1 += r1[k * C + c];
+    }
+  __syncthreads();
+  const float4 ns = nst[(size_t)b * C + c];   // mean, rstd, mhat, tinv
+  const double Gc = s0, Gx = s1;
+  const double al = alpha[c], gm = gamma[c];
+  const double dmh = al * gm * Gc;
+  if (gi == 0) r0[c] = dmh * ns.z;
+  __syncthreads();
+  for (int s = C / 2; s > 0; s >>= 1) {
+    if (gi == 0 && c < s) r0[c] += r0[c + s];
+    __syncthreads();
+  }
+  const double A = r0[0];
+  const double du = (double)ns.w * (dmh - (double)ns.z * A / (C - 1));
+  if (gi == 0) r1[c] = du;
+  __syncthreads();
+  for (int s = C / 2; s > 0; s >>= 1) {
+    if (gi == 0 && c < s) r1[c] += r1[c + s];
+    __syncthreads();
+  }
+  if (gi != 0) return;
+  const double dmu = du - r1[0] / C;
+  // dh = k1*g + k2*(h - mean) + k3: centring h before the product keeps the cancellation
+  // between the xhat and mean terms out of float32
+  const double rs = ns.y;
+  const double k1 = gm * rs;
+  const double k2 = -gm * rs * rs * Gx / N;
+  const double k3 = -gm * rs * Gc / N + dmu / N;
+  coef[(size_t)b * C + c] = make_float4((float)k1, (float)k2, (float)k3, ns.x);
+  float* pp = ppart + ((size_t)b * C + c) * 3;
+  pp[0] = (float)(gm * (double)ns.z * Gc);          // d alpha
+  pp[1] = (float)(Gx + al * (double)ns.z * Gc);     // d gamma
+  pp[2] = (float)Gc;                                // d beta
+}
+
+// parameter gradients = sum over the images of the per-image partials (fixed order)
+__global__ void inpp_bwd_params_kernel(const float* __restrict__ ppart, int B, int C, float* __restrict__ dalpha,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, g = 0.0, be = 0.0;
   for (int b = 0; b < B; ++b) {
-    double s0 = 0.0, s1 = 0.0;
-    for (int k = gi; k < ngrp; k += Gt) {
-      const float2 v = part[((size_t)b * ngrp + k) * C + c];
-      s0 += v.x;
-      s1 += v.y;
-    }
-    r0[tid] = s0;
-    r1[tid] = s1;
-    __syncthreads();
-    if (gi == 0) {
-      for (int k = 1; k < Gt; ++k) {
-        s0 += r0[k * C + c];
-        s1 += r1[k * C + c];
-      }
-    }
-    __syncthreads();
-    const float4 ns = nst[(size_t)b * C + c];   // mean, rstd, mhat, tinv
-    const double Gc = s0, Gx = s1;
-    const double al = alpha[c], gm = gamma[c];
-    const double dmh = al * gm * Gc;
-    if (gi == 0) {
-      r0[c] = dmh * ns.z;
-    }
-    __syncthreads();
-    for (int s = C / 2; s > 0; s >>= 1) {
-      if (gi == 0 && c < s) r0[c] += r0[c + s];
-      __syncthreads();
-    }
-    const double A = r0[0];
-    __syncthreads();
-    const double du = (double)ns.w * (dmh - (double)ns.z * A / (C - 1));
-    if (gi == 0) r1[c] = du;
-    __syncthreads();
-    for (int s = C / 2; s > 0; s >>= 1) {
-      if (gi == 0 && c < s) r1[c] += r1[c + s];
-      __syncthreads();
-    }
-    const double dmu = du - r1[0] / C;
-    __syncthreads();
-    if (gi == 0) {
-      const double rs = ns.y, mu = ns.x;
-      // dh = k1*g + k2*(h - mean) + k3: centring h before the product keeps the cancellation
-      // between the xhat and mean terms out of float32
-      const double k1 = gm * rs;
-      const double k2 = -gm * rs * rs * Gx / N;
-      const double k3 = -gm * rs * Gc / N + dmu / N;
-      coef[(size_t)b * C + c] = make_float4((float)k1, (float)k2, (float)k3, (float)mu);
-      acc_g += Gx + al * (double)ns.z * Gc;
-      acc_b += Gc;
-      acc_a += gm * (double)ns.z * Gc;
-    }
+    const float* pp = ppart + ((size_t)b * C + c) * 3;
+    a += pp[0];
+    g += pp[1];
+    be += pp[2];
   }
-  if (gi == 0) {
-    dalpha[c] = (float)acc_a;
-    dgamma[c] = (float)acc_g;
-    dbeta[c] = (float)acc_b;
-  }
+  dalpha[c] = (float)a;
+  dgamma[c] = (float)g;
+  dbeta[c] = (float)be;
 }
 
 // out = k1*g + k2*(h - mean) + k3 (+ r1) (+ r2)
@@ -217,15 +219,16 @@ __global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __rest
 static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 256 * 32); }
 
 hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
-                         int HW, int C, float* part, float* coef, float* dalpha, float* dgamma, float* dbeta,
-                         const float* r1, const float* r2, float* out, hipStream_t st) {
+                         int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
+                         float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st) {
   if (HW % 512 || C % 4 || C > 1024 || (256 % (C / 4))) return hipErrorInvalidValue;
   const int ngrp = HW / 512;
   hipLaunchKernelGGL(inpp_bwd_reduce_kernel, dim3(ngrp, B), dim3(256), 0, st, g, h,
                      reinterpret_cast<const float4*>(nst), reinterpret_cast<float2*>(part), HW, C);
-  hipLaunchKernelGGL(inpp_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, reinterpret_cast<const float2*>(part), ngrp,
-                     (float)HW, reinterpret_cast<const float4*>(nst), alpha, gamma, B, C,
-                     reinterpret_cast<float4*>(coef), dalpha, dgamma, dbeta);
+  hipLaunchKernelGGL(inpp_bwd_finalize_kernel, dim3(B), dim3(1024), 0, st, reinterpret_cast<const float2*>(part), ngrp,
+                     (float)HW, reinterpret_cast<const float4*>(nst), alpha, gamma, C, reinterpret_cast<float4*>(coef),
+                     ppart);
+  hipLaunchKernelGGL(inpp_bwd_params_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ppart, B, C, dalpha, dgamma, dbeta);
   const size_t n4 = (size_t)B * HW * C / 4;
   hipLaunchKernelGGL(inpp_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, h,
                      reinterpret_cast<const float4*>(coef), r1, r2, out, HW, C, n4);
@@ -248,57 +251,38 @@ __global__ void unpool_kernel(const float* __restrict__ dout, float* __restrict_
   }
 }
 
-// argmax (0..24, row-major window order, first max wins as torch's max_pool2d) of every 5x5 window
-__global__ void maxpool5_argmax_kernel(const float* __restrict__ in, uint8_t* __restrict__ idx, int H, int W, int C,
-                                       size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = i % C;
-    size_t p = i / C;
+// dst[q] = (res ? res[q] : 0) + sum over the windows p containing q whose argmax (idx, written
+// by the forward maxpool5) is q of dp[p]; 4 channels per thread
+__global__ void maxpool5_bwd_kernel(const float* __restrict__ dp, const uchar4* __restrict__ idx,
+                                    const float* __restrict__ res, float* __restrict__ dst, int H, int W, int C, size_t n4) {
+  const int C4 = C / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    size_t p = i / C4;
     const int x = p % W;
     p /= W;
     const int y = p % H;
     const size_t b = p / H;
-    float m = -INFINITY;
-    int best = 12;
-    for (int dy = -2; dy <= 2; ++dy) {
+    float4 s = res ? reinterpret_cast<const float4*>(res)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int dy = -2; dy <= 2; ++dy) {       // window centre (y+dy, x+dx); q sits at its offset (-dy, -dx)
       const int yy = y + dy;
       if (yy < 0 || yy >= H) continue;
       for (int dx = -2; dx <= 2; ++dx) {
         const int xx = x + dx;
         if (xx < 0 || xx >= W) continue;
-        const float v = in[((b * H + yy) * W + xx) * C + c];
-        if (v > m || v != v) {
-          m = v;
-          best = (dy + 2) * 5 + dx + 2;
+        const size_t j = ((b * H + yy) * W + xx) * C4 + c4;
+        const uchar4 k = idx[j];
+        const unsigned char want = (unsigned char)((2 - dy) * 5 + (2 - dx));
+        if (k.x == want || k.y == want || k.z == want || k.w == want) {
+          const float4 d = reinterpret_cast<const float4*>(dp)[j];
+          if (k.x == want) s.x += d.x;
+          if (k.y == want) s.y += d.y;
+          if (k.z == want) s.z += d.z;
+          if (k.w == want) s.w += d.w;
         }
       }
     }
-    idx[i] = (uint8_t)best;
-  }
-}
-
-// dst[q] = (res ? res[q] : 0) + sum over windows p containing q whose argmax is q of dp[p]
-__global__ void maxpool5_bwd_kernel(const float* __restrict__ dp, const uint8_t* __restrict__ idx,
-                                    const float* __restrict__ res, float* __restrict__ dst, int H, int W, int C, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = i % C;
-    size_t p = i / C;
-    const int x = p % W;
-    p /= W;
-    const int y = p % H;
-    const size_t b = p / H;
-    float s = 0.f;
-    for (int dy = -2; dy <= 2; ++dy) {       // window centre (y+dy, x+dx); q sits at offset (-dy, -dx)
-      const int yy = y + dy;
-      if (yy < 0 || yy >= H) continue;
-      for (int dx = -2; dx <= 2; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= W) continue;
-        const size_t j = ((b * H + yy) * W + xx) * C + c;
-        if (idx[j] == (2 - dy) * 5 + (2 - dx)) s += dp[j];
-      }
-    }
-    dst[i] = res ? res[i] + s : s;
+    reinterpret_cast<float4*>(dst)[i] = s;
   }
 }
 
@@ -378,47 +362,26 @@ __global__ void add_kernel(const float* __restrict__ a, const float* __restrict_
   }
 }
 
-// bias gradient: part[blk][c] = sum over the block's pixels ; then out[c] = sum_blk part
-__global__ __launch_bounds__(256) void chan_sum_kernel(const float* __restrict__ dy, size_t npix, int C,
-                                                       float* __restrict__ part) {
-  __shared__ float red[256 * 4];
-  const int C4 = C / 4, PL = 256 / C4, tid = threadIdx.x, c4 = tid % C4, pl = tid / C4;
-  const size_t per = (npix + gridDim.x - 1) / gridDim.x;
-  const size_t p0 = blockIdx.x * per, p1 = min(npix, p0 + per);
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  for (size_t p = p0 + pl; p < p1; p += PL) {
-    const float4 v = *reinterpret_cast<const float4*>(dy + p * C + c4 * 4);
-    s[0] += v.x; s[1] += v.y; s[2] += v.z; s[3] += v.w;
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) red[(pl * C4 + c4) * 4 + k] = s[k];
-  __syncthreads();
-  for (int i = tid; i < C; i += 256) {
-    float a = 0.f;
-    for (int k = 0; k < PL; ++k) a += red[(k * C4 + i / 4) * 4 + (i & 3)];
-    part[(size_t)blockIdx.x * C + i] = a;
-  }
-}
-
-// out[i] = sum_k part[k*stride + i] (fixed order, f64) ; n outputs, K partial rows
-__global__ void sum_rows_kernel(const float* __restrict__ part, int K, int n, int stride, float* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// out[i] = sum_k part[k*stride + i] (fixed order); block = 32 outputs x 8 K-groups
+__global__ __launch_bounds__(256) void sum_rows_kernel(const float* __restrict__ part, int K, int n, int stride,
+                                                       float* __restrict__ out) {
+  __shared__ double red[8][32];
+  const int il = threadIdx.x & 31, kg = threadIdx.x >> 5;
+  const int i = blockIdx.x * 32 + il;
   double s = 0.0;
-  for (int k = 0; k < K; ++k) s += part[(size_t)k * stride + i];
-  out[i] = (float)s;
+  if (i < n)
+    for (int k = kg; k < K; k += 8) s += part[(size_t)k * stride + i];
+  red[kg][il] = s;
+  __syncthreads();
+  if (kg == 0 && i < n) {
+    for (int g = 1; g < 8; ++g) s += red[g][il];
+    out[i] = (float)s;
+  }
 }
 
 static hipError_t sum_rows(const float* part, int K, int n, int stride, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(sum_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, st, part, K, n, stride, out);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3((n + 31) / 32), dim3(256), 0, st, part, K, n, stride, out);
   return hipGetLastError();
-}
-
-hipError_t chan_sum(const float* dy, size_t npix, int C, float* part, float* out, hipStream_t st) {
-  if (C % 4 || 256 % (C / 4)) return hipErrorInvalidValue;
-  const int nb = 256;
-  hipLaunchKernelGGL(chan_sum_kernel, dim3(nb), dim3(256), 0, st, dy, npix, C, part);
-  return sum_rows(part, nb, C, C, out, st);
 }
 
 hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hipStream_t st) {
@@ -427,11 +390,11 @@ hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hip
   return hipGetLastError();
 }
 
-hipError_t maxpool5_backward(const float* src, const float* dp, const float* res, float* dst, uint8_t* idx, int B, int H,
-                             int W, int C, hipStream_t st) {
-  const size_t n = (size_t)B * H * W * C;
-  hipLaunchKernelGGL(maxpool5_argmax_kernel, dim3(grid_for(n)), dim3(256), 0, st, src, idx, H, W, C, n);
-  hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, st, dp, idx, res, dst, H, W, C, n);
+hipError_t maxpool5_backward(const uint8_t* idx, const float* dp, const float* res, float* dst, int B, int H, int W, int C,
+                             hipStream_t st) {
+  const size_t n4 = (size_t)B * H * W * C / 4;
+  hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dp, reinterpret_cast<const uchar4*>(idx),
+                     res, dst, H, W, C, n4);
   return hipGetLastError();
 }
 
@@ -460,7 +423,7 @@ SDP_DEV float linspace01_t(int i, int n) {
   return i < n / 2 ? step * (float)i : 1.0f - step * (float)(n - 1 - i);
 }
 
-constexpr int BW_ROWS = 8;
+constexpr int BW_ROWS = 32;
 __global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                           float* __restrict__ part, int H, int W) {
   __shared__ float sp[4][3][66];
@@ -564,7 +527,7 @@ __global__ __launch_bounds__(256) void end_dgrad_kernel(const float* __restrict_
   }
 }
 
-constexpr int EW_ROWS = 8;
+constexpr int EW_ROWS = 32;
 __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict__ dscore, const float* __restrict__ sigmas,
                                                         const int64_t* __restrict__ labels, const float* __restrict__ o,
                                                         const float* __restrict__ ss, float* __restrict__ part, int H,

@@ -128,11 +128,13 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
     }
   };
   // registers -> LDS (prologue transform on the input patch, zero padding, bf16 split)
+  float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);   // bias gradient: sum of dy over this thread's pixels
   auto store_tile = [&]() {
 #pragma unroll
     for (int k = 0; k < T::NUD; ++k) {
       const int u = tid + k * 256, px = u >> 5, cv = u & 31;
       put_bf16(dyL, T::DY_PLANE, (cv >> 3) * (128 * 64) + px * 64 + (cv & 7) * 8, rd[k]);
+      bsum = make_float4(bsum.x + rd[k].x, bsum.y + rd[k].y, bsum.z + rd[k].z, bsum.w + rd[k].w);
     }
     const float* ssb = a.pro_ss + (size_t)tb * a.ss_bstride + ci0 * 2;
 #pragma unroll
@@ -197,6 +199,22 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
       });
     }
   }
+  // bias partials (the ci-block-0 workgroups): bpart[split][Cout]; every thread's channel
+  // group is tid & 31, its pixels tid >> 5 -> combine the 8 threads of a group through LDS
+  if (a.bpart && blockIdx.y == 0) {
+    __syncthreads();
+    float4* red = reinterpret_cast<float4*>(lds);
+    red[tid] = bsum;
+    __syncthreads();
+    if (tid < 32) {
+      float4 t = red[tid];
+      for (int k = 1; k < 8; ++k) {
+        const float4 v = red[tid + 32 * k];
+        t = make_float4(t.x + v.x, t.y + v.y, t.z + v.z, t.w + v.w);
+      }
+      *reinterpret_cast<float4*>(a.bpart + (size_t)split * Cout + co0 + tid * 4) = t;
+    }
+  }
   // partials: part[split][tap][Cout][Cin]; accumulator register r of lane l is
   // row (co) (r & 3) + 8 (r >> 2) + 4 (l >> 5), column (ci) l & 31
   static_for<0, NT>([&](auto tc_) {
@@ -208,18 +226,36 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
 #endif
 }
 
-// out[co][ci][tap] (+)= sum_s part[s][tap][co][ci], fixed order over s
-__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                                int S, int NT, int Cout, int Cin, int accumulate) {
+// out[co][ci][tap] (+)= sum_s part[s][tap][co][ci] (fixed order over s); grid.y = tap, and
+// grid.y == NT reduces the bias partials bpart[s][co] into bias_out
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part,
+                                                                const float* __restrict__ bpart, float* __restrict__ out,
+                                                                float* __restrict__ bias_out, int S, int NT, int Cout,
+                                                                int Cin, int accumulate) {
   const int i = blockIdx.x * 256 + threadIdx.x;   // co * Cin + ci
-  if (i >= Cout * Cin) return;
-  const size_t plane = (size_t)Cout * Cin;
-  for (int tap = 0; tap < NT; ++tap) {
+  const int tap = blockIdx.y;
+  if (tap == NT) {
+    if (!bpart || i >= Cout) return;
     float s = 0.f;
-    for (int k = 0; k < S; ++k) s += part[((size_t)k * NT + tap) * plane + i];
-    float* o = out + (size_t)i * NT + tap;
-    *o = accumulate ? *o + s : s;
+    for (int k = 0; k < S; ++k) s += bpart[(size_t)k * Cout + i];
+    bias_out[i] = accumulate ? bias_out[i] + s : s;
+    return;
   }
+  if (i >= Cout * Cin) return;
+  const size_t plane = (size_t)Cout * Cin, step = (size_t)NT * plane;
+  const float* p = part + (size_t)tap * plane + i;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= S; k += 4) {
+    s0 += p[(size_t)k * step];
+    s1 += p[(size_t)(k + 1) * step];
+    s2 += p[(size_t)(k + 2) * step];
+    s3 += p[(size_t)(k + 3) * step];
+  }
+  for (; k < S; ++k) s0 += p[(size_t)k * step];
+  const float s = (s0 + s1) + (s2 + s3);
+  float* o = out + (size_t)i * NT + tap;
+  *o = accumulate ? *o + s : s;
 }
 
 int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks) {
@@ -243,7 +279,8 @@ static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStrea
   return hipGetLastError();
 }
 
-hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, int accumulate, hipStream_t st, const char** why) {
+hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,
+                      const char** why) {
   const int d = a.dil;
   if (a.Cin % 32 || a.Cout % 128) { *why = "wgrad: Cin%32 and Cout%128 required"; return hipErrorInvalidValue; }
   if (a.H % d || a.W % d) { *why = "wgrad: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
@@ -254,6 +291,8 @@ hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, int accumulate,
   if (!a.circular && d != 1) { *why = "wgrad: zero padding only for d=1"; return hipErrorInvalidValue; }
   if (!a.pro_ss) { *why = "wgrad: prologue table missing"; return hipErrorInvalidValue; }
   const int S = wgrad_splits(a.B, a.H, a.W, d, a.Cin, a.Cout, ks);
+  if (bias_out && !a.bpart) { *why = "wgrad: bias gradient needs bpart"; return hipErrorInvalidValue; }
+  if (!bias_out) a.bpart = nullptr;
   if (!a.part || a.part_floats < wgrad_part_floats(S, a.Cin, a.Cout, ks)) {
     *why = "wgrad: partial buffer too small";
     return hipErrorInvalidValue;
@@ -266,8 +305,8 @@ hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, int accumulate,
   }
   if (e != hipSuccess) return e;
   const int n = a.Cout * a.Cin;
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((n + 255) / 256), dim3(256), 0, st, a.part, out, S, ks * ks, a.Cout,
-                     a.Cin, accumulate);
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((n + 255) / 256, ks * ks + 1), dim3(256), 0, st, a.part, a.bpart,
+                     out, bias_out, S, ks * ks, a.Cout, a.Cin, accumulate);
   return hipGetLastError();
 }
 
