@@ -4,7 +4,7 @@
 //   end_conv   : final IN++ affine + ELU prologue, ngf->2 zero-padded 3x3 conv + bias,
 //                / sigmas[y] (ncsnv2.py:510-516), NCHW output.
 //   inpp_finalize : per-tile (mean, M2) -> per-(b,c) InstanceNorm2dPlus scale/shift
-//                (normalization.py:163-176).
+//                (normalization.py:163-176), in two small launches.
 //   maxpool5   : MaxPool2d(5, stride 1, padding 2) of CRPBlock (layers.py:70), NHWC.
 #include "common.h"
 
@@ -134,59 +134,63 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
 
 // ---------------------------------------------------------------- IN++ finalize
 // stats [B][T][C] of float2 (tile mean, tile M2) with `cnt` values per tile -> ss [B][C] of
-// float2 (scale, shift) such that IN++(x) = x*scale + shift.  One 1024-thread block per image:
-// G = 1024/C tile groups x C channels, Chan merge of equal-count partials in float64.
-__global__ __launch_bounds__(1024) void inpp_finalize_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
-                                                             const float* __restrict__ alpha,
-                                                             const float* __restrict__ gamma,
-                                                             const float* __restrict__ beta, float2* __restrict__ ss,
-                                                             float4* __restrict__ nst) {
-  __shared__ double red[1024];
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const int G = blockDim.x / C, g = tid / C, c = tid % C;
+// float2 (scale, shift) such that IN++(x) = x*scale + shift.  Two launches:
+//   inpp_moments : one 256-thread block per (image, 64 channels), 4 tile groups; Chan merge
+//                  of the equal-count partials in float64 -> (mean, biased var) per (b, c)
+//   inpp_ss      : one block per image over its C channels: m = mean_c(mean), v = unbiased
+//                  var_c(mean) (normalization.py:164-166), then the affine of every channel
+__global__ __launch_bounds__(256) void inpp_moments_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
+                                                           double2* __restrict__ mv) {
+  __shared__ double red[256];
+  const int cb = C / 64;
+  const int b = blockIdx.x / cb, c = (blockIdx.x % cb) * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
   const float2* st = stats + (size_t)b * T * C + c;
   double sm = 0.0;
-#pragma unroll 8
-  for (int t = g; t < T; t += G) sm += st[(size_t)t * C].x;
-  red[tid] = sm;
+#pragma unroll 4
+  for (int t = g; t < T; t += 4) sm += st[(size_t)t * C].x;
+  red[threadIdx.x] = sm;
   __syncthreads();
-  if (g == 0) {
-    for (int k = 1; k < G; ++k) sm += red[k * C + c];
-    red[c] = sm / T;
-  }
-  __syncthreads();
-  const double mean = red[c];
+  const double mean = (red[threadIdx.x & 63] + red[64 + (threadIdx.x & 63)] + red[128 + (threadIdx.x & 63)] +
+                       red[192 + (threadIdx.x & 63)]) / T;
   __syncthreads();
   double m2 = 0.0;
-#pragma unroll 8
-  for (int t = g; t < T; t += G) {
+#pragma unroll 4
+  for (int t = g; t < T; t += 4) {
     const float2 v = st[(size_t)t * C];
     const double dm = (double)v.x - mean;
     m2 += (double)v.y + dm * dm * cnt;
   }
-  red[tid] = m2;
+  red[threadIdx.x] = m2;
   __syncthreads();
-  if (g == 0)
-    for (int k = 1; k < G; ++k) m2 += red[k * C + c];
-  __syncthreads();
-  // m = mean_c(mean), v = unbiased var_c(mean)       (normalization.py:164-166)
-  if (g == 0) red[c] = mean;
+  if (g == 0) {
+    m2 = red[threadIdx.x] + red[64 + threadIdx.x] + red[128 + threadIdx.x] + red[192 + threadIdx.x];
+    mv[(size_t)b * C + c] = make_double2(mean, m2 / ((double)T * cnt));   // biased (nn.InstanceNorm2d)
+  }
+}
+
+__global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict__ mv, int C,
+                                                       const float* __restrict__ alpha, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float2* __restrict__ ss,
+                                                       float4* __restrict__ nst) {
+  __shared__ double red[1024];
+  const int b = blockIdx.x, c = threadIdx.x;
+  const double2 m_v = mv[(size_t)b * C + c];
+  const double mean = m_v.x, var = m_v.y;
+  red[c] = mean;
   __syncthreads();
   for (int s = C / 2; s > 0; s >>= 1) {
-    if (g == 0 && c < s) red[c] += red[c + s];
+    if (c < s) red[c] += red[c + s];
     __syncthreads();
   }
   const double m = red[0] / C;
   __syncthreads();
-  if (g == 0) red[c] = (mean - m) * (mean - m);
+  red[c] = (mean - m) * (mean - m);
   __syncthreads();
   for (int s = C / 2; s > 0; s >>= 1) {
-    if (g == 0 && c < s) red[c] += red[c + s];
+    if (c < s) red[c] += red[c + s];
     __syncthreads();
   }
-  if (g != 0) return;
   const double v = red[0] / (C - 1);
-  const double var = m2 / ((double)T * cnt);          // biased (nn.InstanceNorm2d)
   const double inv = 1.0 / sqrt(var + 1e-5);
   const double mn = (mean - m) / sqrt(v + 1e-5);
   const double gm = gamma[c];
@@ -198,37 +202,67 @@ __global__ __launch_bounds__(1024) void inpp_finalize_kernel(const float2* __res
 }
 
 // ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
+// Separable: a thread owns 4 channels of one column over MP_ROWS output rows; it takes the
+// 5-wide horizontal max of every input row it needs (MP_ROWS + 4 of them) once and slides a
+// 5-row window over them -> 5*(MP_ROWS+4)/MP_ROWS loads per output instead of 25.
 // idx (training): window position 0..24 of the max in row-major window order, the first one
-// on ties -- the index torch's max_pool2d keeps for its backward
+// on ties (strict > along the row, then strict > down the rows) -- the index torch's
+// max_pool2d keeps for its backward.  -inf padding never wins.
+constexpr int MP_ROWS = 16;
 __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                        uchar4* __restrict__ idx, int B, int H, int W, int C) {
-  const int C4 = C / 4;
-  const size_t n = (size_t)B * H * W * C4;
+  const int C4 = C / 4, RB = (H + MP_ROWS - 1) / MP_ROWS;
+  const size_t n = (size_t)B * RB * W * C4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const int c4 = i % C4;
     size_t p = i / C4;
     const int x = p % W;
     p /= W;
-    const int y = p % H;
-    const int b = p / H;
-    float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    uchar4 bi = make_uchar4(12, 12, 12, 12);
-    for (int dy = -2; dy <= 2; ++dy) {
-      const int yy = y + dy;
-      if (yy < 0 || yy >= H) continue;
+    const int rb = p % RB;
+    const int b = p / RB;
+    const int y0 = rb * MP_ROWS, y1 = min(H, y0 + MP_ROWS);
+    float4 hm[5];          // horizontal maxima of rows y-2 .. y+2 (ring)
+    uchar4 hc[5];          // their column positions dx+2
+    auto hrow = [&](int yy, float4& m, uchar4& c) {
+      m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      c = make_uchar4(2, 2, 2, 2);
+      if (yy < 0 || yy >= H) return;
+      const float* row = in + (((size_t)b * H + yy) * W) * C + c4 * 4;
+#pragma unroll
       for (int dx = -2; dx <= 2; ++dx) {
         const int xx = x + dx;
         if (xx < 0 || xx >= W) continue;
-        const float4 v = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
-        const unsigned char k = (unsigned char)((dy + 2) * 5 + dx + 2);
-        if (v.x > m.x) { m.x = v.x; bi.x = k; }
-        if (v.y > m.y) { m.y = v.y; bi.y = k; }
-        if (v.z > m.z) { m.z = v.z; bi.z = k; }
-        if (v.w > m.w) { m.w = v.w; bi.w = k; }
+        const float4 v = *reinterpret_cast<const float4*>(row + (size_t)xx * C);
+        const unsigned char k = (unsigned char)(dx + 2);
+        if (v.x > m.x) { m.x = v.x; c.x = k; }
+        if (v.y > m.y) { m.y = v.y; c.y = k; }
+        if (v.z > m.z) { m.z = v.z; c.z = k; }
+        if (v.w > m.w) { m.w = v.w; c.w = k; }
+      }
+    };
+#pragma unroll
+    for (int k = 0; k < 4; ++k) hrow(y0 - 2 + k, hm[k], hc[k]);
+    for (int y = y0; y < y1; ++y) {
+      hrow(y + 2, hm[4], hc[4]);
+      float4 m = hm[0];
+      uchar4 bi = make_uchar4(hc[0].x, hc[0].y, hc[0].z, hc[0].w);   // row 0 of the window
+#pragma unroll
+      for (int r = 1; r < 5; ++r) {
+        const unsigned char ro = (unsigned char)(5 * r);
+        if (hm[r].x > m.x) { m.x = hm[r].x; bi.x = ro + hc[r].x; }
+        if (hm[r].y > m.y) { m.y = hm[r].y; bi.y = ro + hc[r].y; }
+        if (hm[r].z > m.z) { m.z = hm[r].z; bi.z = ro + hc[r].z; }
+        if (hm[r].w > m.w) { m.w = hm[r].w; bi.w = ro + hc[r].w; }
+      }
+      const size_t o = (((size_t)b * H + y) * W + x) * C4 + c4;
+      reinterpret_cast<float4*>(out)[o] = m;
+      if (idx) idx[o] = bi;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hm[r] = hm[r + 1];
+        hc[r] = hc[r + 1];
       }
     }
-    *reinterpret_cast<float4*>(out + i * 4) = m;
-    if (idx) idx[i] = bi;
   }
 }
 
@@ -247,14 +281,18 @@ hipError_t end_conv(const float* in, const float* ss, const float* w, const floa
 }
 
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
-                         const float* beta, float* ss, hipStream_t st, float* nst) {
-  hipLaunchKernelGGL(inpp_finalize_kernel, dim3(B), dim3(1024), 0, st, reinterpret_cast<const float2*>(stats), T, cnt, C,
-                     alpha, gamma, beta, reinterpret_cast<float2*>(ss), reinterpret_cast<float4*>(nst));
+                         const float* beta, float* ss, hipStream_t st, float* nst, void* scratch) {
+  if (C % 64 || C > 1024 || (C & (C - 1))) return hipErrorInvalidValue;
+  double2* mv = reinterpret_cast<double2*>(scratch);
+  hipLaunchKernelGGL(inpp_moments_kernel, dim3(B * (C / 64)), dim3(256), 0, st, reinterpret_cast<const float2*>(stats), T,
+                     cnt, C, mv);
+  hipLaunchKernelGGL(inpp_ss_kernel, dim3(B), dim3(C), 0, st, mv, C, alpha, gamma, beta, reinterpret_cast<float2*>(ss),
+                     reinterpret_cast<float4*>(nst));
   return hipGetLastError();
 }
 
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
-  const size_t n = (size_t)B * H * W * (C / 4);
+  const size_t n = (size_t)B * ((H + MP_ROWS - 1) / MP_ROWS) * W * (C / 4);
   const int grid = (int)std::min<size_t>((n + 255) / 256, 256 * 16);
   hipLaunchKernelGGL(maxpool5_kernel, dim3(grid), dim3(256), 0, st, in, out, reinterpret_cast<uchar4*>(idx), B, H, W, C);
   return hipGetLastError();

@@ -9,8 +9,9 @@ hipError_t begin_conv(const float* x, const float* w, const float* bias, float* 
                       hipStream_t st);
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st);
+// scratch: B*C*16 bytes (per-(b,c) float64 mean and variance)
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
-                         const float* beta, float* ss, hipStream_t st, float* nst = nullptr);
+                         const float* beta, float* ss, hipStream_t st, float* nst, void* scratch);
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx = nullptr);
 hipError_t langevin_step(float* x, const float* g, const float* ref, const int32_t* mask, const float* noise,
                          uint64_t seed, uint64_t offset, float step, float nscale, float gref, int n2n, int B, int C,

@@ -30,6 +30,7 @@ struct Fwd {
   hipStream_t st;
   float* stats;
   float* ss;
+  float* mv;     // inpp_finalize scratch
 
   struct Opt {
     int pro = PRO_NONE;        // prologue
@@ -92,7 +93,7 @@ struct Fwd {
   // stats (written by the previous conv) -> scale/shift of InstanceNorm2dPlus `nkey`
   void norm(const std::string& nkey, int T, float cnt, int C) {
     chk(inpp_finalize(stats, B, T, cnt, C, net->P(nkey + ".alpha"), net->P(nkey + ".gamma"), net->P(nkey + ".beta"), ss,
-                      st),
+                      st, nullptr, mv),
         "inpp_finalize");
   }
   static int tiles(const Buf& b) { return b.H * b.W / 128; }
@@ -190,9 +191,10 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
     if (p > end) throw std::runtime_error("workspace too small");
     return q;
   };
-  Fwd f{net, B, st, nullptr, nullptr};
+  Fwd f{net, B, st, nullptr, nullptr, nullptr};
   f.stats = take((size_t)B * (H * W / 64) * C2 * 2);
   f.ss = take((size_t)B * C2 * 2);
+  f.mv = take((size_t)B * C2 * 4);
   auto full = [&]() { return Buf{take(F), H, W, C}; };
   auto half = [&]() { return Buf{take(Q), h, w, C2}; };
   Buf L1 = full(), FA = full(), FB = full(), FC = full(), FD = full(), FE = full();
@@ -268,7 +270,7 @@ static size_t workspace_bytes(const sdp_net* net, int B) {
   const int H = net->d.H, W = net->d.W, C = net->d.ngf, C2 = 2 * C;
   const size_t F = (size_t)B * H * W * C, Q = (size_t)B * (H / 2) * (W / 2) * C2;
   auto r = [](size_t n) { return ((n * 4 + 255) / 256) * 256; };
-  return r((size_t)B * (H * W / 64) * C2 * 2) + r((size_t)B * C2 * 2) + 6 * r(F) + 8 * r(Q);
+  return r((size_t)B * (H * W / 64) * C2 * 2) + r((size_t)B * C2 * 2) + r((size_t)B * C2 * 4) + 6 * r(F) + 8 * r(Q);
 }
 
 // ------------------------------------------------------------------------------ C ABI

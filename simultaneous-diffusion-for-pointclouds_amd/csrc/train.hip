@@ -38,6 +38,7 @@ struct TrainPlan {
   std::map<std::string, float*> fl;   // saved per-norm tables: "<key>#ss", "<key>#nst"
   std::map<std::string, uint8_t*> idxs;  // saved maxpool argmax indices
   float* stats = nullptr;
+  float* mvs = nullptr;               // inpp_finalize scratch
   float* xin = nullptr;               // copy of the forward input [B,2,H,W]
   int64_t* lab = nullptr;             // copy of the labels
   // backward scratch
@@ -125,7 +126,7 @@ struct TrainPlan {
     fl[nkey + "#ss"] = ss;
     fl[nkey + "#nst"] = nst;
     if (dry) return;
-    ok(inpp_finalize(stats, B, T, cnt, c, P(nkey + ".alpha"), P(nkey + ".gamma"), P(nkey + ".beta"), ss, st, nst),
+    ok(inpp_finalize(stats, B, T, cnt, c, P(nkey + ".alpha"), P(nkey + ".gamma"), P(nkey + ".beta"), ss, st, nst, mvs),
        "inpp_finalize " + nkey);
   }
   static int tiles(const T4& t) { return t.H * t.W / 128; }
@@ -267,6 +268,7 @@ struct TrainPlan {
       ok(hipMemcpyAsync(lab, labels, (size_t)B * 8, hipMemcpyDeviceToDevice, st), "copy labels");
     }
     stats = take((size_t)B * (H * W / 64) * 2 * C * 2);
+    mvs = take((size_t)B * 2 * C * 4);
     T4 x0 = mk(H, W, C);
     if (!dry)
       ok(begin_conv(xin, P("begin_conv.weight"), P("begin_conv.bias"), x0.p, stats, B, H, W, st), "begin_conv");
