@@ -19,6 +19,7 @@
  *   sdp_dsm_loss           anneal_dsm_score_estimation_with_mask            losses/dsm.py:67-119
  *   sdp_net_backward       loss.backward()                                  runners/ncsn_runner_kitti_simultaneous.py:230
  *   sdp_adam_ema_step      optimizer.step() (Adam, losses/__init__.py:10-20) + EMAHelper.update (models/ema.py:16-21)
+ *   sdp_range_project      point_cloud_to_range_image                       datasets/lidar_utils.py:54-347
  */
 #ifndef SDP_H
 #define SDP_H
@@ -146,6 +147,17 @@ int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_ou
                           const uint8_t* exist, const uint8_t* sky, const int32_t* refmask,
                           const sdp_merge_params* params, const uint32_t* absmax_bits,
                           float* new_images, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- point cloud -> range image (data front end; datasets/lidar_utils.py:54-347) --------
+ * points: DEVICE float64 [N][stride] (x, y, z[, intensity]); origin: HOST float64 [3].
+ * Outputs (DEVICE, [H][W], already flipped in both axes like the reference): depth float64
+ * (maxRange 2057.701 where empty), intensity float64 (optional, needs has_intensity),
+ * obfuscation u8, sky u8 (all 0, as the reference clears it), index int64 (optional, -1 empty).
+ * The nearest point per pixel wins; equal depths keep the lowest point index.               */
+int sdp_range_project_workspace_size(int H, int W, size_t* bytes);
+int sdp_range_project(const double* points, int N, int stride, int has_intensity, const double* origin,
+                      int H, int W, double* depth, double* intensity, uint8_t* obfuscation, uint8_t* sky,
+                      int64_t* index, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

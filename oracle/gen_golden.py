@@ -270,11 +270,26 @@ def gen_dsm():
          grad_keys=np.array(list(gn.keys())), grad_norms=np.array(list(gn.values())))
 
 
+def gen_projection():
+    """point_cloud_to_range_image (datasets/lidar_utils.py:54-347) on synthetic clouds, with
+    remission -- imported by file path (datasets/__init__.py needs torchvision)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("lidar_utils", os.path.join(REF, "datasets", "lidar_utils.py"))
+    lu = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lu)
+    for tag, (n, origin) in GI.PROJECTION_CASES.items():
+        pc = GI.projection_cloud(tag, n)
+        depth, inten, obf, _, sky, index = lu.point_cloud_to_range_image(pc, np.array(origin), True)
+        save(f"projection_{tag}.npz", depth=depth, intensity=inten.astype(np.float32), obf=obf, sky=sky,
+             index=index.astype(np.int32))
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    what = sys.argv[1:] or ["exist", "scorenet", "ops", "langevin", "merge", "allforone", "config1", "e2e", "dsm"]
+    what = sys.argv[1:] or ["exist", "scorenet", "ops", "langevin", "merge", "allforone", "config1", "e2e", "dsm",
+                            "projection"]
     _ref_imports()
     for w in what:
         {"exist": gen_exist, "scorenet": gen_scorenet, "ops": gen_ops, "langevin": gen_langevin,
          "merge": gen_merge, "allforone": gen_allforone, "config1": gen_config1, "e2e": gen_kitti_e2e,
-         "dsm": gen_dsm}[w]()
+         "dsm": gen_dsm, "projection": gen_projection}[w]()

@@ -94,3 +94,28 @@ def merge_case(tag: str, B: int, H: int, W: int, sigma_mod: float = 1.0, neg_fra
 
 def noise(tag: str, k: int, shape) -> np.ndarray:
     return rng(f"noise-{tag}-{k}").standard_normal(shape).astype(np.float32)
+
+
+def projection_cloud(tag: str, n: int = 60000) -> np.ndarray:
+    """Synthetic LiDAR-like point cloud [n, 4] float64 (x, y, z, intensity): a ground plane,
+    two walls, boxes and free clutter around the origin -- the input shape
+    datasets/kitti360_im_8Batch.py:199 hands to point_cloud_to_range_image."""
+    r = rng("projection_" + tag)
+    k = n // 4
+    ang = r.uniform(-np.pi, np.pi, k)
+    rad = np.sqrt(r.uniform(1.0, 45.0 ** 2, k))
+    ground = np.stack([rad * np.cos(ang), rad * np.sin(ang), -1.73 + r.normal(0, 0.02, k)], 1)
+    wy = np.where(r.random(k) < 0.5, -8.0, 8.0)
+    walls = np.stack([r.uniform(-40, 40, k), wy + r.normal(0, 0.05, k), r.uniform(-1.73, 3.0, k)], 1)
+    bc = r.uniform(-20, 20, (12, 2))
+    bi = r.integers(0, 12, k)
+    boxes = np.stack([bc[bi, 0] + r.uniform(-1.5, 1.5, k), bc[bi, 1] + r.uniform(-1.5, 1.5, k),
+                      r.uniform(-1.73, 0.5, k)], 1)
+    m = n - 3 * k
+    clutter = np.stack([r.uniform(-60, 60, m), r.uniform(-60, 60, m), r.uniform(-3, 8, m)], 1)
+    xyz = np.concatenate([ground, walls, boxes, clutter], 0)
+    inten = r.uniform(0, 1, n).astype(np.float32).astype(np.float64)
+    return np.ascontiguousarray(np.concatenate([xyz, inten[:, None]], 1))
+
+
+PROJECTION_CASES = {"scene_o0": (60000, (0.0, 0.0, 0.0)), "scene_off": (60000, (2.5, -1.25, 0.4))}

@@ -194,3 +194,16 @@ def test_dsm_loss_and_gradients_oracle_matches_reference(params128):
     assert set(keys) == set(grads)
     for k, gn in zip(keys, f["grad_norms"]):
         assert abs(grads[k].norm().item() - gn) <= 1e-4 * gn + 1e-6, k
+
+
+@pytest.mark.parametrize("tag", sorted(GI.PROJECTION_CASES))
+def test_projection_oracle_matches_reference(tag):
+    """oracle/projection_ref.py == datasets/lidar_utils.py:point_cloud_to_range_image, bit for bit."""
+    from oracle import projection_ref as PR
+    n, origin = GI.PROJECTION_CASES[tag]
+    f = _g(f"projection_{tag}.npz")
+    d, inten, obf, _, sky, idx = PR.point_cloud_to_range_image(GI.projection_cloud(tag, n), np.array(origin), True)
+    assert np.array_equal(d, f["depth"])
+    assert np.array_equal(inten.astype(np.float32), f["intensity"])
+    assert np.array_equal(obf, f["obf"]) and np.array_equal(sky, f["sky"])
+    assert np.array_equal(idx.astype(np.int32), f["index"])
