@@ -67,7 +67,8 @@ struct ConvTile {
                                                                 //   staging unit has a pixel slot)
   static constexpr int RAW_BYTES = NU * 256 * 16;               // raw fp32 patch landed by LDS-DMA
   static constexpr int PIPE_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
-  static constexpr int LDS_BYTES = PIPE_BYTES;
+  static constexpr int EPI_BYTES = WM * 64 * (NTILE + 8) * 4;   // LDS-staged epilogue (one half)
+  static constexpr int LDS_BYTES = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
@@ -413,142 +414,311 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   }
 
   SDP_T(3);
-  // ------------------------------------------------------------------ epilogue
-  // Straight from the accumulators, no LDS round trip: register r of fragment (mb, nb) of
-  // lane l holds pixel m = (r&3) + 8(r>>2) + 4(l>>5) of the fragment's 32-pixel row segment
-  // and output channel l&31 of its 32-channel block, so every wave store writes two 128-B
-  // runs of channels.  ConvMeanPool's 2x2 mean pairs registers r, r+1 (columns) and fragments
-  // mb, mb + TC/32 (rows) inside a lane.  Bias, bilinear upsample-add, the backward elu'
-  // factor, residual, the CRP second output and ELU are applied on the way; InstanceNorm++
-  // statistics: each wave holds the whole 128-pixel statistics group of its channels, so a
-  // two-pass (mean, M2) over the lane's values + a Chan merge with lane l^32 gives them.
-  __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
-  {
+  if (a.dact) {
+    // data-gradient launches (training): the LDS-staged epilogue -- its 16-B pixel-row
+    // accesses of the elu' operand and the residual gradient beat per-channel 4-B accesses
+    // ------------------------------------------------------------------ epilogue
+    // The accumulators go through LDS (the patch/raw buffers are free now) in two halves of
+    // 64 pixels per wave, so the output is written as whole pixel rows -- every thread owns 4
+    // consecutive channels of a pixel, every store/load is 16 B and a wave instruction covers
+    // 1 KiB (Cout 256) or two 512-B rows -- with bias, 2x2 mean-pool, residual, bilinear
+    // upsample-add, the CRP second output, ELU and the InstanceNorm++ statistics applied on
+    // the way.
+    __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
+    __syncthreads();
+    constexpr int SROW = T::NTILE + 8;               // staged row stride (floats): conflict-free writes
+    constexpr int SP = WM * 64;                      // staged pixels per half
+    constexpr int CG = T::NTILE / 4;                 // 16-B channel groups per pixel
+    constexpr int PL = 256 / CG;                     // threads per channel group
+    constexpr int NPO = POOL ? SP / 4 : SP;          // output pixels per half
+    static_assert(SP * SROW * 4 <= T::LDS_BYTES, "epilogue staging fits the LDS");
+    float* stage = reinterpret_cast<float*>(lds);
+    const int cg = tid % CG, pl = tid / CG;
+    const int co0 = n0 + cg * 4;                     // this thread's 4 output channels
+    const float4 bias4 = a.bias ? ld4(a.bias + co0) : make_float4(0.f, 0.f, 0.f, 0.f);
     const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
-    const size_t bo = (size_t)b * Ho * Wo * Cout;
-    const int img_bytes = Ho * Wo * Cout * 4;
-    // buffer resources over this image of every epilogue tensor: per-element byte offsets are
-    // a per-fragment VGPR base + a wave-uniform (SGPR) register offset
-    auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p ? p + bo : a.out + bo), 0, img_bytes, 0x00020000); };
-    const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), xrs = rs(a.aux), o2rs = rs(a.out2), r2rs = rs(a.res2);
-    const int lhalf = lane >> 5, lcol = lane & 31;
-    constexpr int CB = TC / 32;                      // fragments per tile row
-    constexpr int NV = POOL ? 16 : 64;               // values per lane per channel block
-    // value i: fragment f = i / PER, register step k = i % PER
-    constexpr int PER = POOL ? 8 : 16;
-    // byte offset step between consecutive output pixels of a fragment row (wave-uniform)
-    const int xs = (POOL ? 1 : d) * Cout * 4;
-    static_for<0, 2>([&](auto nbc) {
-      constexpr int nb = decltype(nbc)::value;
-      const int co = n0 + wn * 64 + nb * 32 + lcol;
-      const float bias = a.bias ? a.bias[co] : 0.f;
-      int vbase[POOL ? CB : 4];                        // byte offset of the fragment's pixel m = 4*lhalf
-      static_for<0, (POOL ? CB : 4)>([&](auto fc) {
-        constexpr int f = decltype(fc)::value;
-        if constexpr (POOL) {
-          vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 32) >> 1) + 2 * lhalf) * Cout + co) * 4;
-        } else {
-          constexpr int mr = f / CB, mc = (f % CB) * 32;
-          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lhalf) * d + ph_c;
-          vbase[f] = ((y * Wo + x) * Cout + co) * 4;
-        }
+    float* outb = a.out + (size_t)b * Ho * Wo * Cout;
+    // shifted sums per (stats group, channel): K = the thread's first value
+    float4 sK[WM], s1[WM], s2[WM];
+    int sn[WM];
+    static_for<0, WM>([&](auto g) {
+      sK[g] = make_float4(0.f, 0.f, 0.f, 0.f); s1[g] = sK[g]; s2[g] = sK[g]; sn[g] = 0;
+    });
+    static_for<0, 2>([&](auto hc) {
+      constexpr int h = decltype(hc)::value;
+      // ---- stage this half's accumulators: wave (wm, wn), fragments mb of the half
+      static_for<0, 2>([&](auto ic) {
+        constexpr int mb = POOL ? (h + 2 * decltype(ic)::value) : (2 * h + decltype(ic)::value);
+        constexpr int q0 = decltype(ic)::value * 32;
+        static_for<0, 2>([&](auto nbc) {
+          constexpr int nb = decltype(nbc)::value;
+          float* dst = stage + (wm * 64 + q0 + 4 * (lane >> 5)) * SROW + wn * 64 + nb * 32 + (lane & 31);
+  #pragma unroll
+          for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * SROW] = acc[mb][nb][r];
+        });
       });
-      // pixel index (within the fragment row, relative to 4*lhalf) of value step k
-      auto mstep = [](int k) { return POOL ? ((((k & 1) * 2 + (k >> 1) * 4) & 3) + 8 * (((k & 1) * 2 + (k >> 1) * 4) >> 2)) / 2
-                                           : (k & 3) + 8 * (k >> 2); };
-      float v[NV];
-      if constexpr (POOL) {
-        static_for<0, CB>([&](auto mbc) {
-          constexpr int mb = decltype(mbc)::value;
-          static_for<0, 8>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            constexpr int r = (k & 1) * 2 + (k >> 1) * 4;          // r & 3 in {0, 2}
-            const float a00 = acc[mb][nb][r], a01 = acc[mb][nb][r + 1];
-            const float a10 = acc[mb + CB][nb][r], a11 = acc[mb + CB][nb][r + 1];
-            v[mb * 8 + k] = ((((a00 + bias) + (a10 + bias)) + (a01 + bias)) + (a11 + bias)) / 4.0f;  // layers.py:310-312
-          });
-        });
-      } else {
-        static_for<0, 4>([&](auto mbc) {
-          constexpr int mb = decltype(mbc)::value;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) v[mb * 16 + r] = acc[mb][nb][r] + bias;
-        });
-      }
-      if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor (non-pooled)
-        const int Hi = a.H / 2, Wi = a.W / 2;
-        const float shh = (float)(Hi - 1) / (float)(a.H - 1), sww = (float)(Wi - 1) / (float)(a.W - 1);
-        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co;
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-          const int f = i / PER, k = i % PER;
-          const int mr = f / CB, mc = (f % CB) * 32;
-          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lhalf + mstep(k)) * d + ph_c;
-          const float fy = shh * (float)y, fx = sww * (float)x;
+      __syncthreads();
+      // ---- row phase: output pixels j = pl, pl + PL, ... of this half
+  #pragma unroll 2
+      for (int j = pl; j < NPO; j += PL) {
+        float4 v;
+        int y, x, g;
+        if constexpr (POOL) {
+          // staged pixel s = row*32 + col over rows 0/1 and columns [32h, 32h+32)
+          const float* s0 = stage + (2 * j) * SROW + cg * 4;
+          const float4 o00 = ld4(s0), o01 = ld4(s0 + SROW), o10 = ld4(s0 + 32 * SROW), o11 = ld4(s0 + 33 * SROW);
+          auto pool1 = [&](float a00, float a10, float a01, float a11, float bb) {
+            return ((((a00 + bb) + (a10 + bb)) + (a01 + bb)) + (a11 + bb)) / 4.0f;  // layers.py:310-312
+          };
+          v.x = pool1(o00.x, o10.x, o01.x, o11.x, bias4.x);
+          v.y = pool1(o00.y, o10.y, o01.y, o11.y, bias4.y);
+          v.z = pool1(o00.z, o10.z, o01.z, o11.z, bias4.z);
+          v.w = pool1(o00.w, o10.w, o01.w, o11.w, bias4.w);
+          y = (sr0 + wrow0) >> 1;
+          x = (sc0 + 32 * h + 2 * j) >> 1;
+          g = 0;
+        } else {
+          const float4 o = ld4(stage + j * SROW + cg * 4);
+          v = make_float4(o.x + bias4.x, o.y + bias4.y, o.z + bias4.z, o.w + bias4.w);
+          const int ws = j >> 6, q = j & 63;                 // staged pixel -> (wave row block, pixel)
+          const int mb = 2 * h + (q >> 5);
+          const int row = ws * T::RW + mb / (TC / 32), col = (mb % (TC / 32)) * 32 + (q & 31);
+          y = (sr0 + row) * d + ph_r;
+          x = (sc0 + col) * d + ph_c;
+          g = ws;
+        }
+        const size_t oidx = ((size_t)y * Wo + x) * Cout + co0;
+        if (a.up) {
+          // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor at (y, x)
+          const int Hi = a.H / 2, Wi = a.W / 2;
+          const float sh = (float)(Hi - 1) / (float)(a.H - 1), sw = (float)(Wi - 1) / (float)(a.W - 1);
+          const float fy = sh * (float)y, fx = sw * (float)x;
           const int y0 = (int)fy, x0 = (int)fx;
           const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
           const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
-          const float v00 = ub[((size_t)y0 * Wi + x0) * Cout], v01 = ub[((size_t)y0 * Wi + x0 + xp) * Cout];
-          const float v10 = ub[((size_t)(y0 + yp) * Wi + x0) * Cout];
-          const float v11 = ub[((size_t)(y0 + yp) * Wi + x0 + xp) * Cout];
-          v[i] = v[i] + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
+          const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co0;
+          const float4 v00 = ld4(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = ld4(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
+          const float4 v10 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
+          const float4 v11 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
+          auto bil = [&](float a00, float a01, float a10, float a11) {
+            return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+          };
+          v.x = v.x + bil(v00.x, v01.x, v10.x, v11.x);
+          v.y = v.y + bil(v00.y, v01.y, v10.y, v11.y);
+          v.z = v.z + bil(v00.z, v01.z, v10.z, v11.z);
+          v.w = v.w + bil(v00.w, v01.w, v10.w, v11.w);
         }
-      }
-#define SDP_EPI_OFF(i) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(mstep((i) % PER) * xs)
-      if (a.dact) {
-        float esc = 1.f, esh = 0.f;
-        if (a.dact == 3) {
-          esc = a.epi_ss[((size_t)b * Cout + co) * 2];
-          esh = a.epi_ss[((size_t)b * Cout + co) * 2 + 1];
+        const size_t bo = (size_t)b * Ho * Wo * Cout;
+        if (a.dact) {
+          // backward: scale by the derivative of the ELU that followed this tensor in the forward
+          //   1: aux = pre-activation h          elu'(h) = h > 0 ? 1 : e^h
+          //   2: aux = post-activation ELU(h)    elu'    = y > 0 ? 1 : y + 1
+          //   3: aux = InstanceNorm++ input h, z = h*scale + shift (epi_ss)  elu'(z)
+          float4 h4 = ld4(a.aux + bo + oidx);
+          if (a.dact == 3) {
+            const float4 s0 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2), s1 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2 + 4);
+            h4 = make_float4(fmaf(h4.x, s0.x, s0.y), fmaf(h4.y, s0.z, s0.w), fmaf(h4.z, s1.x, s1.y), fmaf(h4.w, s1.z, s1.w));
+          }
+          v = make_float4(v.x * elu_grad(h4.x, a.dact), v.y * elu_grad(h4.y, a.dact), v.z * elu_grad(h4.z, a.dact),
+                          v.w * elu_grad(h4.w, a.dact));
         }
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-          float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI_OFF(i), 0));
-          if (a.dact == 3) h = fmaf(h, esc, esh);
-          v[i] = v[i] * elu_grad(h, a.dact);
+        if (a.res) {
+          const float4 r4 = ld4(a.res + bo + oidx);
+          v = make_float4(r4.x + v.x, r4.y + v.y, r4.z + v.z, r4.w + v.w);
         }
-      }
-      if (a.res) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, SDP_EPI_OFF(i), 0)) + v[i];
-      }
-      if (a.out2) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-          const float r2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI_OFF(i), 0));
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2), o2rs, SDP_EPI_OFF(i), 0);
+        if (a.out2) {
+          const float4 r4 = ld4(a.res2 + bo + oidx);
+          *reinterpret_cast<float4*>(a.out2 + bo + oidx) = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
         }
+        if (a.epi_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
+        if constexpr (!(SDP_KO & 16)) *reinterpret_cast<float4*>(outb + oidx) = v;
+        static_for<0, WM>([&](auto gc) {
+          constexpr int gg = decltype(gc)::value;
+          if (gg == g) {
+            if (sn[gg] == 0) sK[gg] = v;
+            const float4 dv = make_float4(v.x - sK[gg].x, v.y - sK[gg].y, v.z - sK[gg].z, v.w - sK[gg].w);
+            s1[gg] = make_float4(s1[gg].x + dv.x, s1[gg].y + dv.y, s1[gg].z + dv.z, s1[gg].w + dv.w);
+            s2[gg] = make_float4(fmaf(dv.x, dv.x, s2[gg].x), fmaf(dv.y, dv.y, s2[gg].y), fmaf(dv.z, dv.z, s2[gg].z),
+                                 fmaf(dv.w, dv.w, s2[gg].w));
+            ++sn[gg];
+          }
+        });
       }
-      if (a.epi_elu) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = elu(v[i]);
-      }
-      if constexpr (!(SDP_KO & 16)) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI_OFF(i), 0);
-      }
-#undef SDP_EPI_OFF
-      if (a.stats) {
-        float sum = 0.f;
-#pragma unroll
-        for (int i = 0; i < NV; ++i) sum += v[i];
-        const float mean_l = sum * (1.0f / NV);
-        float m2_l = 0.f;
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-          const float dv = v[i] - mean_l;
-          m2_l = fmaf(dv, dv, m2_l);
-        }
-        const float mean_p = __shfl_xor(mean_l, 32), m2_p = __shfl_xor(m2_l, 32);
-        const float dm = mean_l - mean_p;
-        const float mean = 0.5f * (mean_l + mean_p);
-        const float m2 = m2_l + m2_p + dm * dm * (0.5f * NV);
-        if (lhalf == 0) {
-          float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile * WM + wm) * Cout + co;
-          *st = make_float2(mean, m2);
-        }
-      }
+      __syncthreads();   // staging buffer reused by the next half / the statistics
     });
+
+    if (a.stats) {
+      // per-thread partials -> (mean, M2) in LDS, then a Chan merge over the PL threads of a
+      // channel group; one 128-pixel statistics group per wave row block (WM)
+      float2* part = reinterpret_cast<float2*>(lds);   // [WM][PL][NTILE]
+      static_for<0, WM>([&](auto gc) {
+        constexpr int gg = decltype(gc)::value;
+        const float n = (float)sn[gg], inv = sn[gg] ? 1.f / n : 0.f;
+        const float k4[4] = {sK[gg].x, sK[gg].y, sK[gg].z, sK[gg].w};
+        const float a4[4] = {s1[gg].x, s1[gg].y, s1[gg].z, s1[gg].w};
+        const float q4[4] = {s2[gg].x, s2[gg].y, s2[gg].z, s2[gg].w};
+  #pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float mean = k4[c] + a4[c] * inv;
+          const float m2 = fmaxf(q4[c] - a4[c] * a4[c] * inv, 0.f);
+          part[(gg * PL + pl) * T::NTILE + cg * 4 + c] = make_float2(mean, m2);
+        }
+      });
+      __syncthreads();
+      constexpr int PER = (POOL ? 32 : 128) / PL;      // values per thread per statistics group
+      for (int i = tid; i < WM * T::NTILE; i += 256) {
+        const int gg = i / T::NTILE, co = i % T::NTILE;
+        float mean = 0.f;
+        for (int k = 0; k < PL; ++k) mean += part[(gg * PL + k) * T::NTILE + co].x;
+        mean *= 1.f / PL;
+        float m2 = 0.f;
+        for (int k = 0; k < PL; ++k) {
+          const float2 pk = part[(gg * PL + k) * T::NTILE + co];
+          const float dm = pk.x - mean;
+          m2 += pk.y + (float)PER * dm * dm;
+        }
+        float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile * WM + gg) * Cout + n0 + co;
+        *st = make_float2(mean, m2);
+      }
+    }
+  } else {
+    // ------------------------------------------------------------------ epilogue
+    // Straight from the accumulators, no LDS round trip: register r of fragment (mb, nb) of
+    // lane l holds pixel m = (r&3) + 8(r>>2) + 4(l>>5) of the fragment's 32-pixel row segment
+    // and output channel l&31 of its 32-channel block, so every wave store writes two 128-B
+    // runs of channels.  ConvMeanPool's 2x2 mean pairs registers r, r+1 (columns) and fragments
+    // mb, mb + TC/32 (rows) inside a lane.  Bias, bilinear upsample-add, the backward elu'
+    // factor, residual, the CRP second output and ELU are applied on the way; InstanceNorm++
+    // statistics: each wave holds the whole 128-pixel statistics group of its channels, so a
+    // two-pass (mean, M2) over the lane's values + a Chan merge with lane l^32 gives them.
+    __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
+    {
+      const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
+      const size_t bo = (size_t)b * Ho * Wo * Cout;
+      const int img_bytes = Ho * Wo * Cout * 4;
+      // buffer resources over this image of every epilogue tensor: per-element byte offsets are
+      // a per-fragment VGPR base + a wave-uniform (SGPR) register offset
+      auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p ? p + bo : a.out + bo), 0, img_bytes, 0x00020000); };
+      const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), xrs = rs(a.aux), o2rs = rs(a.out2), r2rs = rs(a.res2);
+      const int lhalf = lane >> 5, lcol = lane & 31;
+      constexpr int CB = TC / 32;                      // fragments per tile row
+      constexpr int NV = POOL ? 16 : 64;               // values per lane per channel block
+      // value i: fragment f = i / PER, register step k = i % PER
+      constexpr int PER = POOL ? 8 : 16;
+      // byte offset step between consecutive output pixels of a fragment row (wave-uniform)
+      const int xs = (POOL ? 1 : d) * Cout * 4;
+      static_for<0, 2>([&](auto nbc) {
+        constexpr int nb = decltype(nbc)::value;
+        const int co = n0 + wn * 64 + nb * 32 + lcol;
+        const float bias = a.bias ? a.bias[co] : 0.f;
+        int vbase[POOL ? CB : 4];                        // byte offset of the fragment's pixel m = 4*lhalf
+        static_for<0, (POOL ? CB : 4)>([&](auto fc) {
+          constexpr int f = decltype(fc)::value;
+          if constexpr (POOL) {
+            vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 32) >> 1) + 2 * lhalf) * Cout + co) * 4;
+          } else {
+            constexpr int mr = f / CB, mc = (f % CB) * 32;
+            const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lhalf) * d + ph_c;
+            vbase[f] = ((y * Wo + x) * Cout + co) * 4;
+          }
+        });
+        // pixel index (within the fragment row, relative to 4*lhalf) of value step k
+        auto mstep = [](int k) { return POOL ? ((((k & 1) * 2 + (k >> 1) * 4) & 3) + 8 * (((k & 1) * 2 + (k >> 1) * 4) >> 2)) / 2
+                                             : (k & 3) + 8 * (k >> 2); };
+        float v[NV];
+        if constexpr (POOL) {
+          static_for<0, CB>([&](auto mbc) {
+            constexpr int mb = decltype(mbc)::value;
+            static_for<0, 8>([&](auto kc) {
+              constexpr int k = decltype(kc)::value;
+              constexpr int r = (k & 1) * 2 + (k >> 1) * 4;          // r & 3 in {0, 2}
+              const float a00 = acc[mb][nb][r], a01 = acc[mb][nb][r + 1];
+              const float a10 = acc[mb + CB][nb][r], a11 = acc[mb + CB][nb][r + 1];
+              v[mb * 8 + k] = ((((a00 + bias) + (a10 + bias)) + (a01 + bias)) + (a11 + bias)) / 4.0f;  // layers.py:310-312
+            });
+          });
+        } else {
+          static_for<0, 4>([&](auto mbc) {
+            constexpr int mb = decltype(mbc)::value;
+  #pragma unroll
+            for (int r = 0; r < 16; ++r) v[mb * 16 + r] = acc[mb][nb][r] + bias;
+          });
+        }
+        if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor (non-pooled)
+          const int Hi = a.H / 2, Wi = a.W / 2;
+          const float shh = (float)(Hi - 1) / (float)(a.H - 1), sww = (float)(Wi - 1) / (float)(a.W - 1);
+          const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co;
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            const int f = i / PER, k = i % PER;
+            const int mr = f / CB, mc = (f % CB) * 32;
+            const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lhalf + mstep(k)) * d + ph_c;
+            const float fy = shh * (float)y, fx = sww * (float)x;
+            const int y0 = (int)fy, x0 = (int)fx;
+            const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
+            const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+            const float v00 = ub[((size_t)y0 * Wi + x0) * Cout], v01 = ub[((size_t)y0 * Wi + x0 + xp) * Cout];
+            const float v10 = ub[((size_t)(y0 + yp) * Wi + x0) * Cout];
+            const float v11 = ub[((size_t)(y0 + yp) * Wi + x0 + xp) * Cout];
+            v[i] = v[i] + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
+          }
+        }
+  #define SDP_EPI_OFF(i) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(mstep((i) % PER) * xs)
+        if (a.dact) {
+          float esc = 1.f, esh = 0.f;
+          if (a.dact == 3) {
+            esc = a.epi_ss[((size_t)b * Cout + co) * 2];
+            esh = a.epi_ss[((size_t)b * Cout + co) * 2 + 1];
+          }
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI_OFF(i), 0));
+            if (a.dact == 3) h = fmaf(h, esc, esh);
+            v[i] = v[i] * elu_grad(h, a.dact);
+          }
+        }
+        if (a.res) {
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, SDP_EPI_OFF(i), 0)) + v[i];
+        }
+        if (a.out2) {
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            const float r2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI_OFF(i), 0));
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2), o2rs, SDP_EPI_OFF(i), 0);
+          }
+        }
+        if (a.epi_elu) {
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) v[i] = elu(v[i]);
+        }
+        if constexpr (!(SDP_KO & 16)) {
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI_OFF(i), 0);
+        }
+  #undef SDP_EPI_OFF
+        if (a.stats) {
+          float sum = 0.f;
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) sum += v[i];
+          const float mean_l = sum * (1.0f / NV);
+          float m2_l = 0.f;
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            const float dv = v[i] - mean_l;
+            m2_l = fmaf(dv, dv, m2_l);
+          }
+          const float mean_p = __shfl_xor(mean_l, 32), m2_p = __shfl_xor(m2_l, 32);
+          const float dm = mean_l - mean_p;
+          const float mean = 0.5f * (mean_l + mean_p);
+          const float m2 = m2_l + m2_p + dm * dm * (0.5f * NV);
+          if (lhalf == 0) {
+            float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile * WM + wm) * Cout + co;
+            *st = make_float2(mean, m2);
+          }
+        }
+      });
+    }
   }
 #ifdef SDP_TIMING
   SDP_T(4);
