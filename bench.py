@@ -121,7 +121,7 @@ def pmc_traffic(precision, V):
     (tools/pmc_traffic.sh -> profiles/r01_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
     correction) + TCC_EA0_WRREQ bytes, averaged over that kernel's launches at this grid)."""
     mode = {"fp32": 0, "fp32x3": 1, "bf16": 2}[precision]
-    name = f"void sdp::conv_mfma_kernel<{mode}, 1, 64, 3, false, true>(sdp::ConvArgs)"
+    name = f"void sdp::conv_mfma_kernel<{mode}, 1, 64, 3, false, false, true>(sdp::ConvArgs)"
     grid = V * (32 * 512 // 128) * 256
     try:
         with open(os.path.join(REPO, "profiles", "r01_traffic.json")) as f:
