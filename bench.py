@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--workload", choices=["line", "allforone", "train"], default="line")
     ap.add_argument("--views", type=int, default=None, help="views (or training images) per GPU")
     ap.add_argument("--mode", choices=["viewsplit", "megabatch"], default="viewsplit")
+    ap.add_argument("--megabatch-views", type=int, default=None,
+                    help="viewsplit on ONE GPU: merge against a megabatch this large (the other views' images stay "
+                         "fixed) -- one rank's per-step work of BASELINE config 4 (32) without the all-gather")
     ap.add_argument("--precision", choices=["fp32x3", "fp32", "bf16"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -165,7 +168,10 @@ def run_sampling(args, rank, N, dist, dev):
 
     H, W, V = 64, 1024, args.views
     if args.mode == "viewsplit":
-        n_src, aB, o_begin = V * N, V * N, rank * V
+        n_src = V * N if args.megabatch_views is None else args.megabatch_views
+        if args.megabatch_views is not None and (N != 1 or n_src < V):
+            raise SystemExit("--megabatch-views emulates a larger megabatch on one GPU only")
+        aB, o_begin = n_src, rank * V
         sc = scene_views(n_src, H, W)
     else:
         n_src, aB, o_begin = V, V, 0
@@ -252,7 +258,8 @@ def run_sampling(args, rank, N, dist, dev):
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (procedural Line.yml-style scene, random-init NCSN_LiDAR_small weights)",
-            "config": {"workload": wl, "views_per_gpu": V, "megabatch_views": aB, "mode": args.mode,
+            "config": {"workload": wl + (" (megabatch emulated on one GPU)" if args.megabatch_views else ""),
+                       "views_per_gpu": V, "megabatch_views": aB, "mode": args.mode,
                        "conv_arithmetic": args.precision, "parallelism": f"views{N}"},
             "roofline": roof, "cpu_baseline": cpu}
 

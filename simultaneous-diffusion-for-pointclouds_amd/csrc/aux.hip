@@ -24,13 +24,16 @@ SDP_DEV float wave_sum(float v) {
 }
 
 // ---------------------------------------------------------------- begin conv (Cin=4 -> 128)
-// block: 64 output pixels of one row x 128 channels; thread = (pixel, 32-channel quarter)
+// block: 64 output pixels of one row x 128 channels; thread = (pixel, 32-channel quarter).
+// The 64 x 128 result goes through LDS so the stores are whole 512-B pixel rows and the
+// per-(b, c) statistics of the 64-pixel tile are a two-pass column sum (no wave shuffles).
 __global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ out,
                                                          float* __restrict__ stats, int H, int W) {
-  constexpr int CO = 128;
+  constexpr int CO = 128, OS = CO + 4;   // staged row stride (floats)
   __shared__ float sw[36 * CO];          // [ci*9 + tap][co]
   __shared__ float sp[4][3][66];         // prepped input patch [ci][row][col]
+  __shared__ float so[64 * OS];          // staged output [px][co]
   const int tid = threadIdx.x;
   const int tiles_row = W / 64;
   const int tiles_per_img = H * tiles_row;
@@ -64,24 +67,44 @@ __global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict
 #pragma unroll
       for (int j = 0; j < 32; ++j) acc[j] = fmaf(v, wr[j], acc[j]);
     }
-  float* o = out + (((size_t)b * H + y) * W + x0 + px) * CO + cq * 32;
 #pragma unroll
-  for (int j = 0; j < 32; j += 4) *reinterpret_cast<float4*>(o + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
-  // per-(b, co) stats of this 64-pixel tile: one wave holds all 64 pixels of its 32 channels
-#pragma unroll
-  for (int j = 0; j < 32; ++j) {
-    const float mean = wave_sum(acc[j]) * (1.0f / 64.f);
-    const float dv = acc[j] - mean;
-    const float m2 = wave_sum(dv * dv);
-    if (px == j) {
-      float2* st = reinterpret_cast<float2*>(stats) + ((size_t)b * tiles_per_img + tile) * CO + cq * 32 + j;
-      *st = make_float2(mean, m2);
-    }
+  for (int j = 0; j < 32; j += 4)
+    *reinterpret_cast<float4*>(&so[px * OS + cq * 32 + j]) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+  __syncthreads();
+  // rows: 32 threads per pixel row (16 B each), 8 rows per pass
+  float* o = out + (((size_t)b * H + y) * W + x0) * CO;
+  for (int i = tid; i < 64 * 32; i += 256) {
+    const int p = i >> 5, c4 = i & 31;
+    *reinterpret_cast<float4*>(o + (size_t)p * CO + c4 * 4) = *reinterpret_cast<const float4*>(&so[p * OS + c4 * 4]);
+  }
+  // statistics: thread (channel, half) sums 32 pixels, two passes, Chan merge of the halves
+  const int c = tid & 127, hf = tid >> 7;
+  float sm = 0.f;
+  for (int p = hf * 32; p < hf * 32 + 32; ++p) sm += so[p * OS + c];
+  const float mh = sm * (1.f / 32.f);
+  float m2 = 0.f;
+  for (int p = hf * 32; p < hf * 32 + 32; ++p) {
+    const float dv = so[p * OS + c] - mh;
+    m2 = fmaf(dv, dv, m2);
+  }
+  __syncthreads();
+  float2* red = reinterpret_cast<float2*>(sw);
+  red[tid] = make_float2(mh, m2);
+  __syncthreads();
+  if (hf == 0) {
+    const float2 q = red[tid + 128];
+    const float dm = mh - q.x;
+    float2* st = reinterpret_cast<float2*>(stats) + ((size_t)b * tiles_per_img + tile) * CO + c;
+    *st = make_float2(0.5f * (mh + q.x), m2 + q.y + dm * dm * 16.f);
   }
 }
 
 // ---------------------------------------------------------------- end conv (128 -> 2), NCHW out
-// block: 4 rows x 64 cols of output; LDS patch of one 32-channel chunk, pixel stride 33 floats
+// block: 4 rows x 64 cols of output.  Per 32-channel chunk the (6 x 66) patch (IN++ affine +
+// ELU applied on the way in) sits in LDS; wave g (warp-uniform) takes channels 8g..8g+7 of
+// the chunk, each thread one column: a patch column of 6 rows feeds its 4 output rows x 3
+// taps x 2 channels, so every LDS read serves 4 FMAs.  The 4 channel-group partials are
+// summed through LDS at the end.
 __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__ in, const float* __restrict__ ss,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        const float* __restrict__ sigmas, const int64_t* __restrict__ labels,
@@ -89,13 +112,16 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
   constexpr int PS = 33;
   __shared__ float sp[6 * 66 * PS];
   __shared__ float sw[2 * 32 * 9];   // [co][ci][tap] of the chunk
+  __shared__ float red[4][8][64];
   const int tid = threadIdx.x;
   const int tiles_row = W / 64, tiles_per_img = (H / 4) * tiles_row;
   const int b = blockIdx.x / tiles_per_img, tile = blockIdx.x % tiles_per_img;
   const int y0 = (tile / tiles_row) * 4, x0 = (tile % tiles_row) * 64;
-  const int r = tid >> 6, c = tid & 63;
+  const int c = tid & 63, g = tid >> 6;
   const float* ssb = ss + (size_t)b * Cin * 2;
-  float a0 = 0.f, a1 = 0.f;
+  float acc[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = 0.f;
   for (int c0 = 0; c0 < Cin; c0 += 32) {
     __syncthreads();
     for (int i = tid; i < 6 * 66 * 8; i += 256) {
@@ -118,18 +144,41 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
       sw[i] = w[((size_t)co * Cin + c0 + ci) * 9 + tap];
     }
     __syncthreads();
-    for (int ci = 0; ci < 32; ++ci)
+    for (int cj = 0; cj < 8; ++cj) {
+      const int ci = g * 8 + cj;
+      float wv[2][9];
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const float v = sp[((r + tap / 3) * 66 + c + tap % 3) * PS + ci];
-        a0 = fmaf(v, sw[ci * 9 + tap], a0);
-        a1 = fmaf(v, sw[288 + ci * 9 + tap], a1);
+      for (int co = 0; co < 2; ++co)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wv[co][t] = sw[co * 288 + ci * 9 + t];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        float col[6];
+#pragma unroll
+        for (int pr = 0; pr < 6; ++pr) col[pr] = sp[(pr * 66 + c + kw) * PS + ci];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int kh = 0; kh < 3; ++kh) {
+            acc[r][0] = fmaf(col[r + kh], wv[0][kh * 3 + kw], acc[r][0]);
+            acc[r][1] = fmaf(col[r + kh], wv[1][kh * 3 + kw], acc[r][1]);
+          }
       }
+    }
   }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    red[g][2 * r][c] = acc[r][0];
+    red[g][2 * r + 1][c] = acc[r][1];
+  }
+  __syncthreads();
   const float sg = sigmas[labels[b]];
-  const int yy = y0 + r, xx = x0 + c;
-  out[(((size_t)b * 2 + 0) * H + yy) * W + xx] = (a0 + bias[0]) / sg;
-  out[(((size_t)b * 2 + 1) * H + yy) * W + xx] = (a1 + bias[1]) / sg;
+  for (int i = tid; i < 8 * 64; i += 256) {
+    const int k = i >> 6, cc = i & 63, r = k >> 1, co = k & 1;
+    const float v = ((red[0][k][cc] + red[1][k][cc]) + red[2][k][cc]) + red[3][k][cc];
+    out[(((size_t)b * 2 + co) * H + y0 + r) * W + x0 + cc] = (v + bias[co]) / sg;
+  }
 }
 
 // ---------------------------------------------------------------- IN++ finalize

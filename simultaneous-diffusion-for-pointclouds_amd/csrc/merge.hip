@@ -8,6 +8,8 @@
 //     cnt (u32), sum of log-depth codes (f64), sum of intensities (f64),
 //     nearest code (u64 atomicMin on the f64 bits; codes are >= 0 so the order is the
 //     unsigned order), then the lowest source index among the nearest (second pass).
+// Large megabatches scatter into several replicas of the grids (by source view) that a
+// reduce pass folds, so no cell serialises one atomic per source view.
 // A resolve pass turns a cell into the reference's controlled average (mean depth unless
 // it exceeds the nearest depth + allowance), applies the negative-depth flip/roll and crop
 // to the output view, and an apply pass adds cc * (-mask*(x - new)) on unknown pixels
@@ -111,11 +113,32 @@ __global__ __launch_bounds__(256) void merge_accum_kernel(MergeArgs a) {
     const double4 w = a.world[(size_t)(m0 + vl) * HW + p];
     const Proj pr = project(a, w, o);
     if (pr.cell < 0) continue;
-    const size_t ci = (size_t)ol * cells + pr.cell;
+    const size_t ci = ((size_t)(vl % a.nrep) * a.n_out + ol) * cells + pr.cell;
     atomicAdd(&a.cnt[ci], 1u);
     atomicAdd(&a.sumL[ci], pr.code);
     atomicAdd(&a.sumI[ci], (double)a.x[((size_t)(m0 + vl) * 2 + 1) * HW + p]);
     atomicMin(&a.minkey[ci], (unsigned long long)__double_as_longlong(pr.code));
+  }
+}
+
+// ---------------------------------------------------------------- K1b: fold the replicas
+__global__ __launch_bounds__(256) void merge_reduce_kernel(MergeArgs a) {
+  const size_t n = (size_t)a.n_out * a.g.big * a.g.W;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t c = a.cnt[i];
+    double l = a.sumL[i], in = a.sumI[i];
+    unsigned long long mk = a.minkey[i];
+    for (int r = 1; r < a.nrep; ++r) {
+      const size_t j = (size_t)r * n + i;
+      c += a.cnt[j];
+      l = __dadd_rn(l, a.sumL[j]);
+      in = __dadd_rn(in, a.sumI[j]);
+      mk = a.minkey[j] < mk ? a.minkey[j] : mk;
+    }
+    a.cnt[i] = c;
+    a.sumL[i] = l;
+    a.sumI[i] = in;
+    a.minkey[i] = mk;
   }
 }
 
@@ -212,12 +235,19 @@ __global__ __launch_bounds__(256) void merge_apply_kernel(MergeArgs a) {
 
 static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 256 * 16); }
 
+// replicas of the accumulator grids: 1 up to a 7-view megabatch, then one per 2 views, at most 8
+// (measured on one MI355X, 4 output views: a 32-view megabatch costs 25.4 ms/step with one
+// grid, 18.6 ms with 8 replicas, 19.1 ms with 16)
+int merge_replicas(int aB) { return aB < 8 ? 1 : (aB / 2 > 8 ? 8 : aB / 2); }
+
 size_t merge_ws_bytes(int n_src, int n_out, int H, int W) {
   const int big = (int)((25 * 2) * (long)H / 28);
   const size_t cells = (size_t)big * W;
+  const int R = merge_replicas(n_src);                // aB <= n_src
   size_t b = 0;
   b += (size_t)n_src * H * W * sizeof(double4);      // world
-  b += (size_t)n_out * cells * (4 + 4 + 8 + 8 + 8);  // cnt, minidx, sumL, sumI, minkey
+  b += (size_t)R * n_out * cells * (4 + 8 + 8 + 8) + 4 * 256;  // cnt, sumL, sumI, minkey (replicated)
+  b += (size_t)n_out * cells * 4;                    // minidx
   b += (size_t)n_out * 2 * H * W * 4;                // newimg (internal)
   b += (size_t)n_out * H * W;                        // maskimg
   return b + 1024;
@@ -232,12 +262,14 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) & ~size_t(255); return q; };
   a.world = reinterpret_cast<double4*>(take((size_t)a.n_src * H * W * sizeof(double4)));
+  a.nrep = merge_replicas(a.aB);
+  const size_t rc = (size_t)a.nrep * a.n_out * cells;
   char* acc0 = p;
-  a.cnt = reinterpret_cast<uint32_t*>(take((size_t)a.n_out * cells * 4));
-  a.sumL = reinterpret_cast<double*>(take((size_t)a.n_out * cells * 8));
-  a.sumI = reinterpret_cast<double*>(take((size_t)a.n_out * cells * 8));
+  a.cnt = reinterpret_cast<uint32_t*>(take(rc * 4));
+  a.sumL = reinterpret_cast<double*>(take(rc * 8));
+  a.sumI = reinterpret_cast<double*>(take(rc * 8));
   char* ff0 = p;
-  a.minkey = reinterpret_cast<unsigned long long*>(take((size_t)a.n_out * cells * 8));
+  a.minkey = reinterpret_cast<unsigned long long*>(take(rc * 8));
   a.minidx = reinterpret_cast<uint32_t*>(take((size_t)a.n_out * cells * 4));
   char* ff1 = p;
   a.newimg = new_out ? new_out : reinterpret_cast<float*>(take((size_t)a.n_out * 2 * H * W * 4));
@@ -248,6 +280,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   const size_t nw = (size_t)a.n_src * H * W, npair = (size_t)a.n_out * a.aB * H * W, nout = (size_t)a.n_out * H * W;
   hipLaunchKernelGGL(merge_world_kernel, dim3(grid_for(nw)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_accum_kernel, dim3(grid_for(npair)), dim3(256), 0, st, a);
+  if (a.nrep > 1) hipLaunchKernelGGL(merge_reduce_kernel, dim3(grid_for((size_t)a.n_out * cells)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_minidx_kernel, dim3(grid_for(npair)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_resolve_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_apply_kernel, dim3(grid_for(2 * nout)), dim3(256), 0, st, a);

@@ -174,6 +174,18 @@ def test_merge_large_megabatch_vs_oracle():
     assert _close_frac(xc, ox) <= 1e-4
 
 
+@pytest.mark.parametrize("aB,W", [(16, 256), (32, 128)])
+def test_merge_replicated_accumulators_vs_oracle(aB, W):
+    """Megabatches of 16 / 32 views (4 / 8 accumulator replicas folded by merge_reduce; the
+    BASELINE config-4 megabatch is 32) against the oracle restatement."""
+    case = GI.merge_case(f"big{aB}", aB, 64, W)
+    new, xc = _gpu_merge(case, aB, 0.7, 5, 10, 0.01)
+    on, ox = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                           case["fromWorld"], aB, 0.7)
+    assert _close_frac(new, on) <= 1e-4
+    assert _close_frac(xc, ox) <= 1e-4
+
+
 def _noise_feed(tag):
     k = [0]
 
