@@ -252,37 +252,89 @@ __global__ void unpool_kernel(const float* __restrict__ dout, float* __restrict_
 }
 
 // dst[q] = (res ? res[q] : 0) + sum over the windows p containing q whose argmax (idx, written
-// by the forward maxpool5) is q of dp[p]; 4 channels per thread
-__global__ void maxpool5_bwd_kernel(const float* __restrict__ dp, const uchar4* __restrict__ idx,
-                                    const float* __restrict__ res, float* __restrict__ dst, int H, int W, int C, size_t n4) {
-  const int C4 = C / 4;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const int c4 = i % C4;
-    size_t p = i / C4;
-    const int x = p % W;
-    p /= W;
-    const int y = p % H;
-    const size_t b = p / H;
-    float4 s = res ? reinterpret_cast<const float4*>(res)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int dy = -2; dy <= 2; ++dy) {       // window centre (y+dy, x+dx); q sits at its offset (-dy, -dx)
-      const int yy = y + dy;
-      if (yy < 0 || yy >= H) continue;
-      for (int dx = -2; dx <= 2; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= W) continue;
-        const size_t j = ((b * H + yy) * W + xx) * C4 + c4;
-        const uchar4 k = idx[j];
+// by the forward maxpool5) is q of dp[p].  A block owns a 32-column x 32-channel strip of a
+// run of rows and walks down it with a 5-row ring of window centres (idx + dp, 2-column halo)
+// in LDS; the next row is fetched into registers while the current one is summed, so every
+// input byte is read from HBM ~1.1 times and each of the 25 checks per output reads LDS.
+// Positions outside the image get an index no window offset matches.
+constexpr int MPB_W = 32, MPB_CB = 32;
+__global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const float* __restrict__ dp, const uchar4* __restrict__ idx,
+                                                           const float* __restrict__ res, float* __restrict__ dst, int H,
+                                                           int W, int C, int rpb) {
+  constexpr int C4B = MPB_CB / 4, PC = MPB_W + 4, RU = PC * C4B;   // 288 16-B units per ring row
+  __shared__ float4 sd[5 * RU];
+  __shared__ uchar4 si[5 * RU];
+  const int tid = threadIdx.x;
+  const int tw = W / MPB_W, tc = C / MPB_CB, nch = (H + rpb - 1) / rpb;
+  int t = blockIdx.x;
+  const int cb = t % tc;
+  t /= tc;
+  const int tx = t % tw;
+  t /= tw;
+  const int chunk = t % nch;
+  const size_t b = t / nch;
+  const int y0 = chunk * rpb, y1 = min(H, y0 + rpb), x0 = tx * MPB_W, c40 = cb * C4B, C4 = C / 4;
+  const float4* dp4 = reinterpret_cast<const float4*>(dp);
+  float4 d[2];
+  uchar4 k[2];
+  auto fetch = [&](int row) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + h * 256, xx = x0 - 2 + u / C4B;
+      if (u < RU && row >= 0 && row < H && xx >= 0 && xx < W) {
+        const size_t j = ((b * H + row) * W + xx) * C4 + c40 + u % C4B;
+        d[h] = dp4[j];
+        k[h] = idx[j];
+      } else {
+        d[h] = make_float4(0.f, 0.f, 0.f, 0.f);
+        k[h] = make_uchar4(255, 255, 255, 255);
+      }
+    }
+  };
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + h * 256;
+      if (u < RU) {
+        sd[slot * RU + u] = d[h];
+        si[slot * RU + u] = k[h];
+      }
+    }
+  };
+  for (int r = 0; r < 4; ++r) {      // rows y0-2 .. y0+1 -> slots 0..3
+    fetch(y0 - 2 + r);
+    put(r);
+  }
+  fetch(y0 + 2);
+  const int c4 = tid % C4B, col = tid / C4B;   // 32 columns x 8 channel groups
+  int base = 0;                                 // slot of row y-2
+  for (int y = y0; y < y1; ++y) {
+    put(base == 0 ? 4 : base - 1);              // row y+2
+    __syncthreads();
+    fetch(y + 3);
+    const size_t o = ((b * H + y) * W + x0 + col) * C4 + c40 + c4;
+    float4 s = res ? reinterpret_cast<const float4*>(res)[o] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int dy = -2; dy <= 2; ++dy) {
+      int sl = base + dy + 2;
+      sl = sl >= 5 ? sl - 5 : sl;
+#pragma unroll
+      for (int dx = -2; dx <= 2; ++dx) {      // window centre (y+dy, x+dx); q sits at its offset (-dy, -dx)
+        const int u = sl * RU + (col + 2 + dx) * C4B + c4;
+        const uchar4 kk = si[u];
         const unsigned char want = (unsigned char)((2 - dy) * 5 + (2 - dx));
-        if (k.x == want || k.y == want || k.z == want || k.w == want) {
-          const float4 d = reinterpret_cast<const float4*>(dp)[j];
-          if (k.x == want) s.x += d.x;
-          if (k.y == want) s.y += d.y;
-          if (k.z == want) s.z += d.z;
-          if (k.w == want) s.w += d.w;
+        if (kk.x == want || kk.y == want || kk.z == want || kk.w == want) {
+          const float4 dd = sd[u];
+          if (kk.x == want) s.x += dd.x;
+          if (kk.y == want) s.y += dd.y;
+          if (kk.z == want) s.z += dd.z;
+          if (kk.w == want) s.w += dd.w;
         }
       }
     }
-    reinterpret_cast<float4*>(dst)[i] = s;
+    reinterpret_cast<float4*>(dst)[o] = s;
+    base = base == 4 ? 0 : base + 1;
+    __syncthreads();
   }
 }
 
@@ -392,9 +444,13 @@ hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hip
 
 hipError_t maxpool5_backward(const uint8_t* idx, const float* dp, const float* res, float* dst, int B, int H, int W, int C,
                              hipStream_t st) {
-  const size_t n4 = (size_t)B * H * W * C / 4;
-  hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dp, reinterpret_cast<const uchar4*>(idx),
-                     res, dst, H, W, C, n4);
+  if (W % MPB_W || C % MPB_CB) return hipErrorInvalidValue;
+  const int strips = B * (W / MPB_W) * (C / MPB_CB);
+  int rpb = H;                                  // split the rows only as far as needed to fill the chip
+  while (rpb > 8 && (long)strips * ((H + rpb - 1) / rpb) < 2048) rpb = (rpb + 1) / 2;
+  const int nb = strips * ((H + rpb - 1) / rpb);
+  hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(nb), dim3(256), 0, st, dp, reinterpret_cast<const uchar4*>(idx), res, dst,
+                     H, W, C, rpb);
   return hipGetLastError();
 }
 
