@@ -40,6 +40,9 @@ hipError_t dsm_loss(const float* score, const float* noise, const float* mask, c
 hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow, size_t n, float b1, float b2, float eps,
                     float step_size, float bc2_sqrt, float mu, hipStream_t st);
 hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char** why);
+// weight-gradient workgroups per launch (pixel splits x Cin/32 x Cout/128): one round of
+// two workgroups per CU (1024: +2% kernel time and a costlier reduce)
+constexpr int WGRAD_TARGET_BLOCKS = 512;
 int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks);
 size_t wgrad_part_floats(int S, int Cin, int Cout, int ks);
 hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,

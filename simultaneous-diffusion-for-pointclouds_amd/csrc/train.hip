@@ -441,7 +441,7 @@ struct TrainPlan {
     used = fwd_bytes;
     grads = grad_arena;
     // scratch (upper bounds over every layer of the network)
-    wpart_n = (size_t)(512 + 64) * 9 * 128 * 32;
+    wpart_n = (size_t)(WGRAD_TARGET_BLOCKS + 64) * 9 * 128 * 32;   // >= splits x 9 x Cin x Cout for every conv
     wpart = take(wpart_n);
     spart = take((size_t)B * (H * W / 512) * 256 * 2);
     coef = take((size_t)B * 256 * 4);

@@ -47,8 +47,8 @@ struct WgTile {
   static constexpr int A_PLANE = NPIX * 64;             // [px][32 ci] bf16
 };
 
-template <int MODE, int TC, int KS>
-__global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
+template <int MODE, int TC, int KS, int OCC>
+__global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   using T = WgTile<TC, KS>;
   constexpr int NT = KS * KS;
@@ -89,12 +89,11 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
   // base per tensor and the loads go through buffer resources (base in SGPRs, unit offset in a
   // VGPR) -- no per-load address arithmetic.  Tiles whose input patch touches the image border
   // (circular wrap / zero padding) take the general path.
-  int voff_dy[T::NUD], voff_a[T::NUA];
-#pragma unroll
-  for (int k = 0; k < T::NUD; ++k) {
-    const int u = tid + k * 256, px = u >> 5, cv = u & 31;
-    voff_dy[k] = (((px / TC) * d * a.W + (px % TC) * d) * Cout + cv * 4) * 4;
-  }
+  // dy unit k = lane pixel (tid >> 5) + 8k of the tile: one VGPR offset plus a wave-uniform
+  // per-unit step (8 columns, or a row every TC / 8 units) in the SGPR offset
+  const int voff_dy0 = (((tid >> 5) * d) * Cout + (tid & 31) * 4) * 4;
+  const int dy_col8 = 8 * d * Cout * 4, dy_row = d * a.W * Cout * 4;
+  int voff_a[T::NUA];
 #pragma unroll
   for (int k = 0; k < T::NUA; ++k) {
     int u = tid + k * 256;
@@ -103,26 +102,34 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
     voff_a[k] = (((pix / T::PC) * d * a.W + (pix % T::PC) * d) * Cin + cv * 4) * 4;
   }
   const int img_dy_bytes = a.H * a.W * Cout * 4, img_in_bytes = a.H * a.W * Cin * 4;
-  // global -> registers for tile t (decoded into tb, tph_*, tsr0, tsc0)
-  auto load_tile = [&]() {
-    const __amdgpu_buffer_rsrc_t drs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(a.dy + (size_t)tb * a.H * a.W * Cout), 0, img_dy_bytes, 0x00020000);
-    const int dbase = __builtin_amdgcn_readfirstlane((((tsr0 * d + tph_r) * a.W + tsc0 * d + tph_c) * Cout + co0) * 4);
-    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+  // per-tile buffer resources / wave-uniform bases (tile decoded into tb, tph_*, tsr0, tsc0)
+  __amdgpu_buffer_rsrc_t drs, irs;
+  int dbase = 0, ibase = 0;
+  bool interior = false;
+  auto prep_tile = [&]() {
+    drs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.dy + (size_t)tb * a.H * a.W * Cout), 0, img_dy_bytes, 0x00020000);
+    dbase = __builtin_amdgcn_readfirstlane((((tsr0 * d + tph_r) * a.W + tsc0 * d + tph_c) * Cout + co0) * 4);
+    interior = tsr0 >= T::HALO && tsr0 + T::TR + T::HALO <= Hs && tsc0 >= T::HALO && tsc0 + TC + T::HALO <= Ws;
+    irs = __builtin_amdgcn_make_buffer_rsrc((void*)(a.in + (size_t)tb * a.H * a.W * Cin), 0, img_in_bytes, 0x00020000);
+    ibase = __builtin_amdgcn_readfirstlane(
+        ((((tsr0 - T::HALO) * d + tph_r) * a.W + (tsc0 - T::HALO) * d + tph_c) * Cin + ci0) * 4);
+  };
+  // global -> registers, units [KB, KE) of the dy tile / the input patch
+  auto load_dy = [&](auto kb_, auto ke_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
 #pragma unroll
-    for (int k = 0; k < T::NUD; ++k) {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drs, voff_dy[k], dbase, 0);
+    for (int k = KB; k < KE; ++k) {
+      constexpr int KPR = TC / 8;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(drs, voff_dy0, dbase + (k % KPR) * dy_col8 + (k / KPR) * dy_row, 0);
       rd[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
     }
-    const bool interior = tsr0 >= T::HALO && tsr0 + T::TR + T::HALO <= Hs && tsc0 >= T::HALO &&
-                          tsc0 + TC + T::HALO <= Ws;
+  };
+  auto load_a = [&](auto kb_, auto ke_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
     if (interior) {
-      const __amdgpu_buffer_rsrc_t irs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(a.in + (size_t)tb * a.H * a.W * Cin), 0, img_in_bytes, 0x00020000);
-      const int ibase = __builtin_amdgcn_readfirstlane(
-          ((((tsr0 - T::HALO) * d + tph_r) * a.W + (tsc0 - T::HALO) * d + tph_c) * Cin + ci0) * 4);
 #pragma unroll
-      for (int k = 0; k < T::NUA; ++k) {
+      for (int k = KB; k < KE; ++k) {
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(irs, voff_a[k], ibase, 0);
         ra[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
       }
@@ -130,7 +137,7 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
     }
     const float* inb = a.in + (size_t)tb * a.H * a.W * Cin + ci0;
 #pragma unroll
-    for (int k = 0; k < T::NUA; ++k) {
+    for (int k = KB; k < KE; ++k) {
       int u = tid + k * 256;
       u = u < T::NPIX * 8 ? u : 0;
       const int pix = u >> 3, cv = u & 7;
@@ -161,16 +168,23 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
   };
   // registers -> LDS (prologue transform on the input patch, zero padding, bf16 split)
   float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);   // bias gradient: sum of dy over this thread's pixels
-  auto store_tile = [&]() {
+  auto store_dy = [&](auto kb_, auto ke_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
 #pragma unroll
-    for (int k = 0; k < T::NUD; ++k) {
+    for (int k = KB; k < KE; ++k) {
       const int u = tid + k * 256, px = u >> 5, cv = u & 31;
       put_bf16(dyL, T::DY_PLANE, (cv >> 3) * (128 * 64) + px * 64 + (cv & 7) * 8, rd[k]);
       bsum = make_float4(bsum.x + rd[k].x, bsum.y + rd[k].y, bsum.z + rd[k].z, bsum.w + rd[k].w);
     }
+    // keep the bias sums here: sunk past the k loop they hold the previous tile's registers
+    // alive beside the next tile's loads (64 VGPRs of copies)
+    asm volatile("" : "+v"(bsum.x), "+v"(bsum.y), "+v"(bsum.z), "+v"(bsum.w));
+  };
+  auto store_a = [&](auto kb_, auto ke_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
     const float* ssb = a.pro_ss + (size_t)tb * a.ss_bstride + ci0 * 2;
 #pragma unroll
-    for (int k = 0; k < T::NUA; ++k) {
+    for (int k = KB; k < KE; ++k) {
       const int u = tid + k * 256;
       if (u >= T::NPIX * 8) break;
       const int pix = u >> 3, cv = u & 7;
@@ -188,6 +202,26 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
       put_bf16(aL, T::A_PLANE, pix * 64 + cv * 8, v);
     }
   };
+  using I0 = std::integral_constant<int, 0>;
+  using IND = std::integral_constant<int, T::NUD>;
+  using INA = std::integral_constant<int, T::NUA>;
+  // OCC 2: two workgroups per CU take turns (one stages while the other's MFMAs run), so a
+  // tile is staged in chunks of CH units straight through registers, no cross-tile prefetch
+  constexpr int CH = 8;
+  auto stage_chunked = [&]() {
+    static_for<0, (T::NUD + CH - 1) / CH>([&](auto c) {
+      using KB = std::integral_constant<int, decltype(c)::value * CH>;
+      using KE = std::integral_constant<int, (decltype(c)::value * CH + CH < T::NUD ? decltype(c)::value * CH + CH : T::NUD)>;
+      load_dy(KB{}, KE{});
+      store_dy(KB{}, KE{});
+    });
+    static_for<0, (T::NUA + CH - 1) / CH>([&](auto c) {
+      using KB = std::integral_constant<int, decltype(c)::value * CH>;
+      using KE = std::integral_constant<int, (decltype(c)::value * CH + CH < T::NUA ? decltype(c)::value * CH + CH : T::NUA)>;
+      load_a(KB{}, KE{});
+      store_a(KB{}, KE{});
+    });
+  };
 
   // transposed-read lane roles (ds_read_b64_tr_b16, 32x32x16 operand): lane l of 16-lane
   // group G supplies row q = (l & 15) >> 2 (K), columns 4p .. 4p+3, p = l & 3 (M or N)
@@ -197,17 +231,29 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
   const char* dy_rd = dyL + wave * (128 * 64) + mcol * 2;
   const char* a_rd = aL + mcol * 2;
 
-  if (t_begin < t_end) {
+  if (OCC == 1 && t_begin < t_end) {
     decode(t_begin);
-    load_tile();
+    prep_tile();
+    load_dy(I0{}, IND{});
+    load_a(I0{}, INA{});
   }
   for (int t = t_begin; t < t_end; ++t) {
     __syncthreads();
-    store_tile();
-    __syncthreads();
-    if (t + 1 < t_end) {
-      decode(t + 1);
-      load_tile();
+    if constexpr (OCC == 1) {
+      store_dy(I0{}, IND{});
+      store_a(I0{}, INA{});
+      __syncthreads();
+      if (t + 1 < t_end) {
+        decode(t + 1);
+        prep_tile();
+        load_dy(I0{}, IND{});
+        load_a(I0{}, INA{});
+      }
+    } else {
+      decode(t);
+      prep_tile();
+      stage_chunked();
+      __syncthreads();
     }
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {   // 16 pixels per k step
@@ -217,13 +263,23 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_kernel(WgradArgs a) {
         alo = cat8(ds_read_tr(dy_rd + T::DY_PLANE + k0 * 64), ds_read_tr(dy_rd + T::DY_PLANE + k1 * 64));
       // patch pixel of tile pixel k at tap (0, 0)
       const int p0 = (k0 / TC) * T::PC + k0 % TC, p1 = (k1 / TC) * T::PC + k1 % TC;
+      const char* b0 = a_rd + p0 * 64;
+      const char* b1 = a_rd + p1 * 64;
+      auto rd_b = [&](int toff, int plane) { return cat8(ds_read_tr(b0 + plane + toff), ds_read_tr(b1 + plane + toff)); };
+      // B operands one tap ahead, so an MFMA never waits on the LDS read issued just before it
+      bf16x8 bhi_n = rd_b(0, 0), blo_n;
+      if constexpr (MODE == MODE_F32X3) blo_n = rd_b(0, T::A_PLANE);
       static_for<0, NT>([&](auto tc_) {
         constexpr int tap = decltype(tc_)::value;
-        constexpr int toff = (KS == 3 ? (tap / 3) * T::PC + tap % 3 : 0) * 64;
-        const bf16x8 bhi = cat8(ds_read_tr(a_rd + p0 * 64 + toff), ds_read_tr(a_rd + p1 * 64 + toff));
+        const bf16x8 bhi = bhi_n;
+        bf16x8 blo;
+        if constexpr (MODE == MODE_F32X3) blo = blo_n;
+        if constexpr (tap + 1 < NT) {
+          constexpr int toff = (KS == 3 ? ((tap + 1) / 3) * T::PC + (tap + 1) % 3 : 0) * 64;
+          bhi_n = rd_b(toff, 0);
+          if constexpr (MODE == MODE_F32X3) blo_n = rd_b(toff, T::A_PLANE);
+        }
         if constexpr (MODE == MODE_F32X3) {
-          const bf16x8 blo = cat8(ds_read_tr(a_rd + T::A_PLANE + p0 * 64 + toff),
-                                  ds_read_tr(a_rd + T::A_PLANE + p1 * 64 + toff));
           acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[tap], 0, 0, 0);
           acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[tap], 0, 0, 0);
         }
@@ -295,7 +351,7 @@ int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks) {
   const int total = B * (H / d) * (W / d) / 128 * d * d;
   (void)tc;
   const int blocks = (Cin / 32) * (Cout / 128);
-  int S = (512 + blocks - 1) / blocks;
+  int S = (WGRAD_TARGET_BLOCKS + blocks - 1) / blocks;
   S = S < total ? S : total;
   return S < 1 ? 1 : S;
 }
@@ -305,9 +361,10 @@ size_t wgrad_part_floats(int S, int Cin, int Cout, int ks) { return (size_t)S * 
 template <int MODE>
 static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
   dim3 grid(S, a.Cin / 32, a.Cout / 128);
-  if (ks == 1) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 1>), grid, dim3(256), 0, st, a);
-  else if (tc == 64) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3>), grid, dim3(256), 0, st, a);
+  constexpr int OCC = MODE == MODE_BF16 ? 2 : 1;
+  if (ks == 1) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 1, OCC>), grid, dim3(256), 0, st, a);
+  else if (tc == 64) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3, OCC>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3, OCC>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
