@@ -20,6 +20,9 @@
  *   sdp_net_backward       loss.backward()                                  runners/ncsn_runner_kitti_simultaneous.py:230
  *   sdp_adam_ema_step      optimizer.step() (Adam, losses/__init__.py:10-20) + EMAHelper.update (models/ema.py:16-21)
  *   sdp_range_project      point_cloud_to_range_image                       datasets/lidar_utils.py:54-347
+ *   sdp_view_transform     pose chain fromWorld @ (toWorld @ p)             datasets/kitti360_im_8Batch.py:146-190
+ *   sdp_view_gather        scanPoints[index[index >= 0]]                    datasets/kitti360_im_simultenous_densification.py:186-203
+ *   sdp_view_finalize      __getitem__ post-processing of the range images  datasets/kitti360_im_8Batch.py:221-304
  */
 #ifndef SDP_H
 #define SDP_H
@@ -158,6 +161,31 @@ int sdp_range_project_workspace_size(int H, int W, size_t* bytes);
 int sdp_range_project(const double* points, int N, int stride, int has_intensity, const double* origin,
                       int H, int W, double* depth, double* intensity, uint8_t* obfuscation, uint8_t* sky,
                       int64_t* index, void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---- KITTI-360 view rendering (the datasets' __getitem__) --------------
+ * sdp_view_transform: points DEVICE float32 [n][4] (x, y, z, intensity, the .bin layout);
+ *   m1, m2 HOST float64 row-major 4x4 or NULL.  out DEVICE float64 [n][4] =
+ *   (m2 @ (m1 @ [x y z 1]))[:3], intensity -- kitti360_im_8Batch.py:146-190 with m1 = toWorld
+ *   of the scan's pose and m2 = fromWorld of the goal pose; NULL, NULL = float64 widening.
+ * sdp_view_gather: the densification subsample scanPoints[index[index >= 0]] after
+ *   index[:, :blank_cols] = -2 (kitti360_im_simultenous_densification.py:186-203).  index DEVICE
+ *   int64 [H][W] (sdp_range_project output), points DEVICE float32 [N][4]; out DEVICE float64
+ *   [<= H*W][4] in row-major pixel order; *count (DEVICE int) = number written.
+ * sdp_view_finalize: kitti360_im_8Batch.py:221-304 (variant SDP_VIEW_8BATCH),
+ *   kitti360_im_AllForOne.py:253-353 (SDP_VIEW_ALLFORONE), kitti360_im_simultenous_
+ *   densification.py:230-339 (SDP_VIEW_DENSIFICATION; first_view = numberInBatch == 0).
+ *   Inputs are sdp_range_project outputs of the view and of the goal scan ([H][W], DEVICE;
+ *   intensity / goal_intensity only with channels == 2); roll = the random_roll column shift
+ *   or -1.  Outputs DEVICE: real, goal float64 [channels][H][W], notmask u8 [channels][H][W]
+ *   (np.logical_not(mask)), notsky u8 [H][W] (np.logical_not(sky) after the 3-row shift).   */
+enum sdp_view_variant { SDP_VIEW_8BATCH = 0, SDP_VIEW_ALLFORONE = 1, SDP_VIEW_DENSIFICATION = 2 };
+int sdp_view_transform(const float* points, int64_t n, const double* m1, const double* m2, double* out, void* stream);
+int sdp_view_gather(const int64_t* index, int H, int W, int blank_cols, const float* points, double* out, int* count,
+                    void* stream);
+int sdp_view_finalize(const double* depth, const double* intensity, const uint8_t* obfuscation, const uint8_t* sky,
+                      const double* goal_depth, const double* goal_intensity, int H, int W, int channels, int roll,
+                      int variant, int first_view, double* real, uint8_t* notmask, uint8_t* notsky, double* goal,
+                      void* stream);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,9 @@ def parse_args_and_config(argv=None):
     p.add_argument("--ckpt", type=str, default=None, help="LiDARGen checkpoint (list format with EMA shadow)")
     p.add_argument("--precision", type=str, default="fp32x3", choices=["fp32x3", "fp32", "bf16"])
     p.add_argument("--num_batches", type=int, default=1)
+    p.add_argument("--kitti_root", type=str, default=None,
+                   help="KITTI-360 root (the reference's /data/KITTI-360); views rendered on the GPU "
+                        "(sdp.kitti360). Without it the procedural scene of sdp.synthetic is used.")
     args = p.parse_args(argv)
     args.log_path = os.path.join(args.exp, "logs", args.doc)
     path = args.config if os.path.exists(args.config) else os.path.join("configs", args.config)

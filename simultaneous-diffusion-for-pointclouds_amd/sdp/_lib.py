@@ -56,6 +56,9 @@ _SIGS = {
     "sdp_adam_ema_step": (I, [P, P, P, P, P, SZ, F, F, F, F, I, F, P]),
     "sdp_range_project_workspace_size": (I, [I, I, C.POINTER(SZ)]),
     "sdp_range_project": (I, [P, I, I, I, P, I, I, P, P, P, P, P, P, SZ, P]),
+    "sdp_view_transform": (I, [P, C.c_int64, P, P, P, P]),
+    "sdp_view_gather": (I, [P, I, I, I, P, P, P, P]),
+    "sdp_view_finalize": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P]),
     "sdp_langevin_step": (I, [P, P, P, P, P, U64, U64, F, F, F, I, I, I, I, P, P, P]),
     "sdp_axpy_step": (I, [P, P, F, P, P, P, F, I, P]),
     "sdp_merge_workspace_size": (I, [I, I, I, I, C.POINTER(SZ)]),

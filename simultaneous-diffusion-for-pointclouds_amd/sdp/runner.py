@@ -14,8 +14,10 @@ as the reference names them (np.save appends .npy):
 Images are saved as inverse_data_transform (clamp [0,1], datasets/__init__.py:206-215) and
 transposed to [2B',3,H,W] (rows [0,B') depth, [B',2B') intensity, 3 identical channels).
 
-KITTI-360 is not available offline, so the data source is the procedural scene of
-``sdp.synthetic`` (same tensor contract as the dataset's 9-tuple, kitti360_im_8Batch.py:304).
+Data: with ``args.kitti_root`` the views come from the KITTI-360 datasets of sdp.kitti360
+(rendered on the GPU) in the order of the reference's MySampler over the pose file
+(kitti:494-515); otherwise from the procedural scene of ``sdp.synthetic`` (same 9-tuple
+contract, kitti360_im_8Batch.py:304).
 """
 from __future__ import annotations
 
@@ -26,7 +28,7 @@ import time
 import numpy as np
 import torch
 
-from . import synthetic
+from . import kitti360, synthetic
 from .sampling import (anneal_Langevin_dynamics_inpainting,
                        anneal_Langevin_dynamics_inpainting_simultaneous_basic,
                        anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti)
@@ -97,6 +99,20 @@ class Runner:
             net.load_synthetic()
         return net
 
+    def _batch_source(self, ds, B, aB, H, W):
+        """bi -> the DataLoader's 9-tuple for batch bi (kitti:514-538)."""
+        root = getattr(self.args, "kitti_root", None)
+        if not root:
+            return lambda bi: synthetic_batch(bi, B, aB, H, W, seed=getattr(self.args, "seed", 1234))
+        dset = kitti360.get_dataset(ds, None, self.config, split="test", root=root, device=self.device)
+        order = iter(kitti360.MySampler(kitti360.val_size(root, aB), aB, random=False))
+
+        def fetch(bi):
+            b = list(kitti360.collate([dset[next(order)] for _ in range(B)]))
+            b[4], b[5] = b[4].reshape(B, 4, 4), b[5].reshape(B, 4, 4)   # [B,1,4,4] -> [B,4,4]
+            return tuple(b)
+        return fetch
+
     def sample(self):
         c = self.config
         B, aB = c.sampling.batch_size, c.sampling.actualBatchSize
@@ -116,9 +132,10 @@ class Runner:
         end_point, to_add = aB, 0
         if ds == "KITTI360_im_simultaneous_densification":   # AllForOne:553-558
             end_point, to_add = 2, aB - 2
+        fetch = self._batch_source(ds, B, aB, H, W)
         for bi in range(n_batches):
             (ref_full, mask_full, sky_full, idx_full, toWorld_full, fromWorld_full, goal, toOG,
-             save_arr) = synthetic_batch(bi, B, aB, H, W, seed=getattr(self.args, "seed", 1234))
+             save_arr) = fetch(bi)
             save_num = "".join(str(int(save_arr[m * aB])) + "_" for m in range(n_mega))
             np.save(os.path.join(folder, "toWorld_" + save_num), toWorld_full.numpy())
             np.save(os.path.join(folder, "fromWorld_" + save_num), toOG.numpy())

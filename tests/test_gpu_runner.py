@@ -33,3 +33,28 @@ def test_main_sample_small(tmp_path, name):
     last = np.load(out / f"1_0_3__Masked_completion_897.pth.npy")
     known = inp > 0                      # doThis=1 samples all 6 views, in input order
     assert last.shape == inp.shape and np.abs(last[known] - inp[known]).max() < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["HDVMine_Line.yml", "HDVMine_Circle.yml"])
+def test_main_sample_from_kitti_tree(tmp_path, name):
+    """--kitti_root: the batch comes from the GPU-rendered KITTI-360 dataset (sdp.kitti360)."""
+    from kitti_tree import write_tree
+    root = tmp_path / "KITTI-360"
+    write_tree(str(root), n_poses=40, n_points=20000)
+    with open(os.path.join(CFG_DIR, name)) as f:
+        c = yaml.safe_load(f)
+    c["sampling"].update(batch_size=3, actualBatchSize=3, n_steps_each=1)
+    c["data"].update(image_width=256, modifications=c["data"]["modifications"][:3])
+    cfg = tmp_path / "small.yml"
+    cfg.write_text(yaml.safe_dump(c))
+    assert sdp_main.main(["--config", str(cfg), "--sample", "--ni", "--exp", str(tmp_path / "exp"),
+                          "--verbose", "warning", "--kitti_root", str(root)]) == 0
+    out = tmp_path / "exp" / "image_samples" / "images"
+    files = sorted(p.name for p in out.iterdir())
+    masked = [f for f in files if f.startswith("0_") and "Masked_completion" in f]
+    assert masked, files
+    m = np.load(out / masked[0])
+    assert m.shape[1:] == (3, 64, 256) and np.isfinite(m).all() and 0 <= m.min() and m.max() <= 1
+    inp = np.load(out / masked[0].replace("Masked", "Input"))
+    assert inp.max() > 0           # real depth codes reached the sampler
