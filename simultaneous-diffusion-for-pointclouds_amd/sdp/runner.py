@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from . import kitti360, synthetic
+from .imgutil import make_grid, save_image
 from .sampling import (anneal_Langevin_dynamics_inpainting,
                        anneal_Langevin_dynamics_inpainting_simultaneous_basic,
                        anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti)
@@ -99,6 +100,10 @@ class Runner:
             net.load_synthetic()
         return net
 
+    def _png(self, grid_views, name, nrow):
+        """make_grid + save_image of a [2B',3,H,W] layout (kitti:658-661)."""
+        save_image(make_grid(grid_views.detach().float().cpu(), max(nrow, 1)), os.path.join(self.args.image_folder, name))
+
     def _batch_source(self, ds, B, aB, H, W):
         """bi -> the DataLoader's 9-tuple for batch bi (kitti:514-538)."""
         root = getattr(self.args, "kitti_root", None)
@@ -137,6 +142,7 @@ class Runner:
             (ref_full, mask_full, sky_full, idx_full, toWorld_full, fromWorld_full, goal, toOG,
              save_arr) = fetch(bi)
             save_num = "".join(str(int(save_arr[m * aB])) + "_" for m in range(n_mega))
+            png_id = str(bi) if kitti else save_num      # kitti names the PNGs by batchesToDo (kitti:534,661)
             np.save(os.path.join(folder, "toWorld_" + save_num), toWorld_full.numpy())
             np.save(os.path.join(folder, "fromWorld_" + save_num), toOG.numpy())
             for do in range(end_point):
@@ -145,13 +151,14 @@ class Runner:
                 mask = mask_full.int().to(self.device)
                 sky, toWorld, fromWorld = sky_full.clone(), toWorld_full.clone(), fromWorld_full.clone()
                 if do == 0:
-                    np.save(os.path.join(folder, f"{do}_{save_num}_Input_completion_{ck}.pth"),
-                            to_grid_layout(inverse_data_transform(ref_full * mask_full)).numpy())
+                    inp = to_grid_layout(inverse_data_transform(ref_full * mask_full))
+                    self._png(inp, f"{do}_{png_id}_Input_image_grid_{ck}.png", int(np.sqrt(B)))
+                    np.save(os.path.join(folder, f"{do}_{save_num}_Input_completion_{ck}.pth"), inp.numpy())
                     # kitti saves the goal scans (kitti:678-694); AllForOne re-saves the masked
                     # input as "GT" (AllForOne:667-711, the second transpose is skipped) -- kept.
-                    gt = goal if kitti else ref_full * mask_full
-                    np.save(os.path.join(folder, f"{do}_{save_num}_GT_completion_{ck}.pth"),
-                            to_grid_layout(inverse_data_transform(gt)).numpy())
+                    gt = to_grid_layout(inverse_data_transform(goal if kitti else ref_full * mask_full))
+                    self._png(gt, f"{do}_{png_id}_GT_image_grid_{ck}.png", int(np.sqrt(B)))
+                    np.save(os.path.join(folder, f"{do}_{save_num}_GT_completion_{ck}.pth"), gt.numpy())
                     np.save(os.path.join(folder, f"{do}_{save_num}_SKY_{ck}.pth"), sky_full.numpy())
                 baseline = (do == aB - 1) if kitti else (do + to_add == aB - 1)
                 k = do + 2 if (do + to_add) < aB - 2 else aB
@@ -184,10 +191,19 @@ class Runner:
                 time_taken[do] += time.time() - t0
                 logging.info("--- %s seconds --- (doThis %d, %d views)", time_taken[do] / (bi + 1), do, init.shape[0])
                 np.save(os.path.join(folder, f"{do}_{save_num}_TimeTaken.npy"), time_taken[do])
+                # grid width: sqrt of the views sampled (kitti:859-870, AllForOne:946-991)
+                if baseline and not kitti:
+                    nrow = int(np.sqrt(1 * n_mega))
+                elif do + to_add < aB - 2:
+                    nrow = int(np.sqrt((do + 2) * n_mega))
+                else:
+                    nrow = int(np.sqrt(B))
                 sample = inverse_data_transform(outs[-1].view(init.shape[0], c.data.channels, H, W))
+                self._png(to_grid_layout(sample), f"{do}_{png_id}_Masked_image_grid_{ck}.png", nrow)
                 np.save(os.path.join(folder, f"{do}_{save_num}_Masked_completion_{ck}.pth"),
                         to_grid_layout(sample).numpy())
                 if not kitti:   # AllForOne:971-988: all_outputs[-2] (last merge image / denoised)
                     shared = inverse_data_transform(outs[-2].view(init.shape[0], c.data.channels, H, W))
+                    self._png(to_grid_layout(shared), f"{do}_{png_id}_Shared_image_grid_initial{ck}.png", nrow)
                     np.save(os.path.join(folder, f"{do}_{save_num}_Shared_completion_initial{ck}.pth"),
                             to_grid_layout(shared).numpy())

@@ -28,6 +28,9 @@ def test_main_sample_small(tmp_path, name):
         m = np.load(out / f"{d}_0_3__Masked_completion_897.pth.npy")
         assert m.shape == (2 * n, 3, 64, 256)
         assert np.isfinite(m).all() and 0 <= m.min() and m.max() <= 1
+    pngs = sorted(p.name for p in out.glob("*_image_grid_*.png"))
+    assert "0_0_Input_image_grid_897.png" in pngs or "0_0_3__Input_image_grid_897.png" in pngs, pngs
+    assert len([p for p in pngs if "Masked_image_grid" in p]) == 3, pngs
     # the known pixels were written back by the final consistency step
     inp = np.load(out / "0_0_3__Input_completion_897.pth.npy")
     last = np.load(out / f"1_0_3__Masked_completion_897.pth.npy")
