@@ -1,4 +1,6 @@
 // Launchers of the forward convolutions of NCSN_LiDAR_small (kernel: conv_kernel.h).
+#include <cstdlib>
+
 #include "conv_kernel.h"
 
 namespace sdp {
@@ -40,7 +42,12 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (a.H % d || a.W % d) { *why = "conv: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
   const int Hs = a.H / d, Ws = a.W / d;
   // 256-channel outputs: 128 px x 256 Cout tiles; 128-channel outputs: 256 px x 128 Cout
+#ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: SDP_WM=1|2 forces the workgroup shape
+  const char* wm_env = getenv("SDP_WM");
+  const int wm = wm_env ? atoi(wm_env) : ((a.Cout % 256 == 0) ? 1 : 2);
+#else
   const int wm = (a.Cout % 256 == 0) ? 1 : 2;
+#endif
   int tc = (wm == 2) ? 32 : ((Ws % 64 == 0) ? 64 : 32);
   if (ks == 1 || pool) tc = 64;
   const int tr = wm * 128 / tc;
@@ -55,6 +62,7 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (!a.pro_ss) { *why = "conv: prologue scale/shift table missing"; return hipErrorInvalidValue; }
   if (a.Cin > 1024 && a.ss_bstride == 0) { *why = "conv: identity table holds 1024 channels"; return hipErrorInvalidValue; }
 #ifdef SDP_CONV_BENCH_ONLY
+  if (mode == MODE_BF16) return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st);
   return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
 #endif
   switch (mode) {

@@ -1,9 +1,11 @@
 // Standalone timing of one conv_mfma launch shape (diagnostics; links a conv.o built with
-// -DSDP_CONV_BENCH_ONLY [-DSDP_KO=mask]).  Usage: conv_bench Cin Cout H W B [dil] [iters]
+// -DSDP_CONV_BENCH_ONLY [-DSDP_KO=mask]).  Usage: conv_bench Cin Cout H W B [dil] [iters] [mode]
+// (mode: 0 fp32, 1 fp32x3 (default), 2 bf16)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../simultaneous-diffusion-for-pointclouds_amd/csrc/kernels.h"
@@ -13,6 +15,7 @@
 int main(int argc, char** argv) {
   const int Cin = atoi(argv[1]), Cout = atoi(argv[2]), H = atoi(argv[3]), W = atoi(argv[4]), B = atoi(argv[5]);
   const int dil = argc > 6 ? atoi(argv[6]) : 1, iters = argc > 7 ? atoi(argv[7]) : 20;
+  const int mode = argc > 8 ? atoi(argv[8]) : sdp::MODE_F32X3;
   const size_t nin = (size_t)B * H * W * Cin, nout = (size_t)B * H * W * Cout, nw = (size_t)Cout * Cin * 9;
   std::vector<float> h(std::max(nin, nw));
   srand(1);
@@ -26,7 +29,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&stats, (size_t)B * (H * W / 128) * Cout * 2 * 4));
   CK(hipMalloc(&bias, Cout * 4));
   CK(hipMemcpy(in, h.data(), nin * 4, hipMemcpyHostToDevice));
-  CK(hipMemcpy(wf, h.data(), nw * 4, hipMemcpyHostToDevice));   // random bits: timing only
+  // packed weight words: two bf16 halves of small random values (realistic bit toggling --
+  // MFMA power, and so the clock, depends on the operand bits)
+  std::vector<uint32_t> hw(nw);
+  for (auto& v : hw) {
+    float f0 = ((float)rand() / RAND_MAX - 0.5f) * 0.05f, f1 = ((float)rand() / RAND_MAX - 0.5f) * 0.05f;
+    uint32_t b0, b1;
+    memcpy(&b0, &f0, 4);
+    memcpy(&b1, &f1, 4);
+    v = (b0 >> 16) | (b1 & 0xffff0000u);
+  }
+  CK(hipMemcpy(wf, hw.data(), nw * 4, hipMemcpyHostToDevice));
   std::vector<float> sh((size_t)B * Cin * 2);
   for (size_t i = 0; i < sh.size(); i += 2) { sh[i] = 1.f; sh[i + 1] = 0.f; }
   CK(hipMemcpy(ss, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
@@ -44,16 +57,16 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) CK(sdp::conv_mfma(sdp::MODE_F32X3, a, 3, false, 0, &why));
+  for (int i = 0; i < 3; ++i) CK(sdp::conv_mfma(mode, a, 3, false, 0, &why));
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(sdp::conv_mfma(sdp::MODE_F32X3, a, 3, false, 0, &why));
+  for (int i = 0; i < iters; ++i) CK(sdp::conv_mfma(mode, a, 3, false, 0, &why));
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / iters, fl = 2.0 * B * H * W * (double)Cin * Cout * 9;
-  printf("conv %d->%d @%dx%d B=%d d=%d: %.1f us  %.1f TF/s (fp32x3 algorithmic)\n", Cin, Cout, H, W, B, dil, us,
+  printf("conv %d->%d @%dx%d B=%d d=%d mode %d: %.1f us  %.1f TF/s (algorithmic)\n", Cin, Cout, H, W, B, dil, mode, us,
          fl / us * 1e-6);
 #ifdef SDP_TIMING
   std::vector<unsigned long long> d((size_t)nwg_max * 8);

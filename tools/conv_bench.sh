@@ -17,7 +17,7 @@ if [ "${RUN:-0}" = 0 ]; then
 else
   for ko in ${KOS:-0 1 2 4 8 16}; do
     echo "KO=$ko"
-    timeout -k 5 60 tools/_cb/conv_bench_$ko 256 256 32 512 4 1 20
-    timeout -k 5 60 tools/_cb/conv_bench_$ko 128 128 64 1024 4 1 20
+    timeout -k 5 60 tools/_cb/conv_bench_$ko 256 256 32 512 ${B:-4} 1 20 ${MODE:-1}
+    timeout -k 5 60 tools/_cb/conv_bench_$ko 128 128 64 1024 ${B:-4} 1 20 ${MODE:-1}
   done
 fi
