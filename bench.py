@@ -9,6 +9,9 @@ Workloads (--workload):
   train (config 5): one DSM training step of the kitti runner (score-net forward, masked DSM
       loss, backward, gradient all-reduce over RCCL, Adam + EMA, weight re-pack, 5 Langevin
       predictions of the unknown pixels), batch 8 per GPU, bf16.  Prints its own metric.
+  project: one step = the KITTI360_im_8batch __getitem__ compute of a
+      megabatch of 8 views from a 120k-point scan resident in HBM (pose-chain transform, view
+      and goal projections, post-processing).  Prints its own metric.
 
 Modes for line (one process per GPU; torchrun sets RANK/LOCAL_RANK/WORLD_SIZE):
   viewsplit (default): ONE megabatch of 4*N views (Line.yml 4 views on 1 GPU = config 2;
@@ -39,6 +42,9 @@ import torch  # noqa: E402
 
 METRIC = "Langevin denoising steps/sec on 64×1024 range images, 1/2/4/8 MI355X"
 TRAIN_METRIC = "DSM training image-steps/sec on 64×1024 range images (fwd+bwd+Adam+EMA), 1/2/4/8 MI355X"
+PROJECT_METRIC = ("KITTI-360 views rendered/sec (pose chain + view and goal point_cloud_to_range_image + "
+                  "post-processing) at 64×1024, 1/2/4/8 MI355X")
+HBM_PEAK = 8000.0             # GB/s, MI355X_MICROARCH.md
 PEAK = {"fp32": 157.3, "fp32x3": 2500.0 / 3, "bf16": 2500.0}  # dense MFMA TFLOP/s in algorithmic fp32 FLOPs
 FWD_FLOP = 1.2663e12          # score-net forward FLOPs per 64x1024 image
 # Inpainting.yml (HDVMine_Circle.yml) data.modifications + 2 more origins: 8 aux views (config 3)
@@ -51,7 +57,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["line", "allforone", "train"], default="line")
+    ap.add_argument("--workload", choices=["line", "allforone", "train", "project"], default="line")
     ap.add_argument("--views", type=int, default=None, help="views (or training images) per GPU")
     ap.add_argument("--mode", choices=["viewsplit", "megabatch"], default="viewsplit")
     ap.add_argument("--megabatch-views", type=int, default=None,
@@ -62,7 +68,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
     if a.views is None:
-        a.views = {"line": 4, "allforone": 9, "train": 8}[a.workload]
+        a.views = {"line": 4, "allforone": 9, "train": 8, "project": 8}[a.workload]
     if a.precision is None:
         a.precision = "bf16" if a.workload == "train" else "fp32x3"
     if a.workload == "allforone":
@@ -312,6 +318,130 @@ def run_train(args, rank, N, dist, dev):
             "roofline": roof, "cpu_baseline": cpu, "final_loss": float(losses[-1])}
 
 
+def synthetic_scan(n, seed):
+    """A LiDAR-like float32 [n, 4] scan (x, y, z, intensity): ground ring, two walls, boxes, clutter."""
+    r = np.random.default_rng(seed)
+    k = n // 4
+    a = r.uniform(-np.pi, np.pi, k)
+    rad = np.sqrt(r.uniform(1.0, 45.0 ** 2, k))
+    ground = np.stack([rad * np.cos(a), rad * np.sin(a), -1.73 + r.normal(0, 0.02, k)], 1)
+    walls = np.stack([r.uniform(-40, 40, k), np.where(r.random(k) < 0.5, -8.0, 8.0), r.uniform(-1.73, 3.0, k)], 1)
+    bc = r.uniform(-20, 20, (12, 2))
+    bi = r.integers(0, 12, k)
+    boxes = np.stack([bc[bi, 0] + r.uniform(-1.5, 1.5, k), bc[bi, 1] + r.uniform(-1.5, 1.5, k),
+                      r.uniform(-1.73, 0.5, k)], 1)
+    m = n - 3 * k
+    clutter = np.stack([r.uniform(-60, 60, m), r.uniform(-60, 60, m), r.uniform(-3, 8, m)], 1)
+    xyz = np.concatenate([ground, walls, boxes, clutter], 0)
+    return np.concatenate([xyz, r.uniform(0, 1, (n, 1))], 1).astype(np.float32)
+
+
+def view_poses(V, seed):
+    """toWorld of the scan's pose and fromWorld = inv(toWorld of the goal pose 5(k+1) ahead)."""
+    r = np.random.default_rng(seed)
+
+    def pose(k):
+        th = 0.04 * k + r.uniform(-0.01, 0.01)
+        m = np.eye(4)
+        m[:3, :3] = [[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]]
+        m[:3, 3] = [1.7 * k + 100.0, -0.4 * k + 50.0, 110.0]
+        return m
+    return pose(0), [np.linalg.inv(pose(5 * (k + 1))) for k in range(V)]
+
+
+def cpu_baseline_project(H, W, n_pts):
+    """The oracle restatement of one 8batch item's compute (numpy, single-threaded)."""
+    from oracle import kitti_ref
+    scan, goal = synthetic_scan(n_pts, 1), synthetic_scan(n_pts, 2)
+    to_world, from_worlds = view_poses(1, 3)
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        pts = kitti_ref.transform(scan, to_world, from_worlds[0])
+        kitti_ref.render_arrays(pts, goal, np.zeros(3), H, W)
+        n += 1
+        if time.perf_counter() - t0 > 10.0 or n >= 120:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "views/s", "cores": 1, "kind": "port",
+            "sample": f"{n} KITTI360_im_8batch items ({n_pts} points, {H}x{W}) through the numpy restatement "
+                      f"(oracle/kitti_ref.py: np.matmul pose chain, argsort z-buffer projection x2, post), {dt:.2f} s"}
+
+
+def run_project(args, rank, N, dist, dev):
+    from sdp import _lib
+    H, W, V, NP = 64, 1024, args.views, 120000
+    L, st = _lib.lib(), _lib.stream()
+    scan = torch.from_numpy(synthetic_scan(NP, 1 + rank)).to(dev)
+    goal32 = torch.from_numpy(synthetic_scan(NP, 1000 + rank)).to(dev)
+    goal = torch.empty(NP, 4, dtype=torch.float64, device=dev)
+    _lib.check(L.sdp_view_transform(goal32.data_ptr(), NP, None, None, goal.data_ptr(), st), "widen")
+    to_world, from_worlds = view_poses(V, 7 + rank)
+    mats = [(np.ascontiguousarray(to_world), np.ascontiguousarray(f)) for f in from_worlds]
+    n = _lib.SZ()
+    _lib.check(L.sdp_range_project_workspace_size(H, W, _lib.C.byref(n)), "ws")
+    ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
+    o = np.zeros(3)
+    pts = torch.empty(NP, 4, dtype=torch.float64, device=dev)
+    f64 = lambda *s: torch.empty(*s, dtype=torch.float64, device=dev)
+    u8 = lambda *s: torch.empty(*s, dtype=torch.uint8, device=dev)
+    img = dict(d=f64(H, W), i=f64(H, W), o=u8(H, W), s=u8(H, W), x=torch.empty(H, W, dtype=torch.int64, device=dev),
+               gd=f64(H, W), gi=f64(H, W))
+    out = [dict(real=f64(2, H, W), goal=f64(2, H, W), nm=u8(2, H, W), ns=u8(1, H, W)) for _ in range(V)]
+
+    def project(p, d, i, ob, sk, ix):
+        _lib.check(L.sdp_range_project(p.data_ptr(), NP, 4, 1, o.ctypes.data, H, W, d.data_ptr(), i.data_ptr(),
+                                       _lib.ptr(ob), _lib.ptr(sk), _lib.ptr(ix),
+                                       ws.data_ptr(), ws.numel(), st), "project")
+
+    def step(i):
+        for v in range(V):
+            m1, m2 = mats[v]
+            _lib.check(L.sdp_view_transform(scan.data_ptr(), NP, m1.ctypes.data, m2.ctypes.data, pts.data_ptr(), st),
+                       "transform")
+            project(pts, img["d"], img["i"], img["o"], img["s"], img["x"])
+            project(goal, img["gd"], img["gi"], None, None, None)      # goal: depth + intensity only
+            r = out[v]
+            _lib.check(L.sdp_view_finalize(img["d"].data_ptr(), img["i"].data_ptr(), img["o"].data_ptr(),
+                                           img["s"].data_ptr(), img["gd"].data_ptr(), img["gi"].data_ptr(), H, W, 2,
+                                           -1, 0, 1 if v == 0 else 0, r["real"].data_ptr(), r["nm"].data_ptr(),
+                                           r["ns"].data_ptr(), r["goal"].data_ptr(), st), "finalize")
+
+    for i in range(args.warmup):
+        step(i)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    dt = timed(step, argparse.Namespace(warmup=0, steps=args.steps), dist, dev)
+    e1.record()
+    e1.synchronize()
+    dev_ms_per_view = e0.elapsed_time(e1) / (args.steps * V)
+    assert all(bool(torch.isfinite(r["real"]).all()) for r in out)
+    if rank != 0:
+        return None
+    # algorithmic bytes per view: transform 16 B in + 32 B out per point; per projection two
+    # passes over the points (32 B + an 8-B atomic each) and per pixel the winner's 32 B and the
+    # outputs (33 B; the view's also the 10-B sky scan); finalize 34 B in + 35 B out per pixel
+    HW = H * W
+    view_bytes = 48 * NP + 2 * (80 * NP + 65 * HW) + 10 * HW + 69 * HW
+    achieved = view_bytes / (dev_ms_per_view * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+            "kernel": "one view's launch sequence (sdp_view_transform + 2 x sdp_range_project + sdp_view_finalize), "
+                      "HIP events on the launch stream",
+            "algorithmic_bytes_per_view": view_bytes, "avg_view_us": round(dev_ms_per_view * 1e3, 2)}
+    cpu = None
+    if N == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_project(H, W, NP)
+    return {"metric": PROJECT_METRIC, "value": round(N * V * args.steps / dt, 2), "unit": "views/s", "n_gpus": N,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic ({NP}-point LiDAR-like scans, resident in HBM)",
+            "config": {"workload": "KITTI360_im_8batch __getitem__ compute for a megabatch of views "
+                                   "(datasets/kitti360_im_8Batch.py:146-291)", "views_per_gpu": V,
+                       "points_per_scan": NP, "parallelism": f"views{N}"},
+            "roofline": roof, "cpu_baseline": cpu}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -324,6 +454,8 @@ def main():
         torch.distributed.init_process_group("nccl", device_id=dev)
     if args.workload == "train":
         line = run_train(args, rank, world, dist, dev)
+    elif args.workload == "project":
+        line = run_project(args, rank, world, dist, dev)
     else:
         line = run_sampling(args, rank, world, dist, dev)
     if line is not None:

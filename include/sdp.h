@@ -155,7 +155,8 @@ int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_ou
  * points: DEVICE float64 [N][stride] (x, y, z[, intensity]); origin: HOST float64 [3].
  * Outputs (DEVICE, [H][W], already flipped in both axes like the reference): depth float64
  * (maxRange 2057.701 where empty), intensity float64 (optional, needs has_intensity),
- * obfuscation u8, sky u8 (all 0, as the reference clears it), index int64 (optional, -1 empty).
+ * obfuscation u8, sky u8 (all 0, as the reference clears it; both NULL skips the row-sequential
+ * sky/obfuscation scan), index int64 (optional, -1 empty).
  * The nearest point per pixel wins; equal depths keep the lowest point index.               */
 int sdp_range_project_workspace_size(int H, int W, size_t* bytes);
 int sdp_range_project(const double* points, int N, int stride, int has_intensity, const double* origin,

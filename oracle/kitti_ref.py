@@ -129,9 +129,25 @@ def item(root, variant, idx, batch_size, modifications, H=64, W=1024, random_rol
         pts = np.transpose(np.concatenate((pv[:-1], np.expand_dims(inten, 0)), 0))
         origin = np.zeros(3) if variant == 0 else mods[nb]
         ret_to, ret_from = to_world2, from_world
+    real, notmask, notsky, index, goal = render_arrays(pts, goal_pts, origin, H, W, variant, nb,
+                                                       roll_draw=lambda: (rng or np.random).randint(W),
+                                                       random_roll=random_roll)
+    return real, notmask, notsky, index[None], ret_to[None], ret_from[None], goal, to_og, scan_no
+
+
+def render_arrays(pts, goal_pts, origin, H, W, variant=0, nb=0, roll_draw=None, random_roll=False):
+    """The two projections and the post-processing of one item (the compute of 8Batch:199-291)."""
     real, intensity, mask, _, sky, index = point_cloud_to_range_image(pts, origin, True, rowMax=H, colMax=W)
     gd, gi, _, _, _, _ = point_cloud_to_range_image(goal_pts, origin, True, rowMax=H, colMax=W)
-    roll = (rng or np.random).randint(W)
+    roll = roll_draw() if roll_draw is not None else 0
     real, notmask, notsky, goal = _post(real, intensity, mask, sky, gd, gi, H, W, roll if random_roll else None,
                                         variant, nb)
-    return real, notmask, notsky, index[None], ret_to[None], ret_from[None], goal, to_og, scan_no
+    return real, notmask, notsky, index, goal
+
+
+def transform(pts, to_world, from_world):
+    """8Batch:146-190: fromWorld @ (toWorld @ [x y z 1]) with the intensity re-attached."""
+    inten = pts[:, -1]
+    pv = np.concatenate((np.transpose(pts[:, :-1]), np.expand_dims(np.ones_like(inten), 0)), 0)
+    pv = np.matmul(from_world, np.matmul(to_world, pv))
+    return np.transpose(np.concatenate((pv[:-1], np.expand_dims(inten, 0)), 0))

@@ -95,41 +95,68 @@ __global__ void proj_pixel_kernel(const double* __restrict__ pts, int stride, in
   }
 }
 
-// one block of W threads (W <= 1024): rows are sequential, columns parallel
+// one block of W threads (W <= 1024): rows are sequential, columns parallel.  Each thread
+// slides a (row-1, row, row+1) window down its column; the rows are fetched RC at a time into
+// registers (one memory latency per RC rows instead of per row), and the 3-column sum goes
+// through a double-buffered LDS row, so one barrier per row suffices.
+constexpr int SKY_RC = 16;
 __global__ __launch_bounds__(1024) void proj_sky_kernel(const double* __restrict__ xy, int H, int W,
                                                         uint8_t* __restrict__ obf, uint8_t* __restrict__ sky) {
-  __shared__ int e[1024 + 2];
+  __shared__ int e[2][1024 + 2];
   const int c = threadIdx.x;
+  const bool act = c < W;
   double md = PROJ_MAX_RANGE;
   bool prev_sky = true;                 // rows 0 and 1 are sky (L285-287)
-  if (c < W) {
+  if (act) {
     obf[c] = 0;
     obf[W + c] = 0;
   }
-  if (c == 0) {
-    e[0] = 0;
-    e[W + 1] = 0;
+  if (c < 2) {
+    e[c][0] = 0;
+    e[c][W + 1] = 0;
   }
-  for (int row = 2; row < H - 1; ++row) {
-    int ev = 0;
-    if (c < W) {
-      const double x0 = xy[(size_t)row * W + c];
-      obf[(size_t)row * W + c] = x0 > md + 5 ? 1 : 0;
-      ev = (x0 != md) + (xy[(size_t)(row - 1) * W + c] != md) + (xy[(size_t)(row + 1) * W + c] != md);
-      e[c + 1] = ev;
+  double xm1 = act ? xy[(size_t)W + c] : 0.0, x0 = act ? xy[(size_t)2 * W + c] : 0.0;   // rows 1, 2
+  for (int r0 = 2; r0 < H - 1; r0 += SKY_RC) {
+    double nx[SKY_RC];                  // rows r0+1 .. r0+RC
+#pragma unroll
+    for (int k = 0; k < SKY_RC; ++k) {
+      const int rr = r0 + 1 + k;
+      nx[k] = (act && rr < H) ? xy[(size_t)rr * W + c] : 0.0;
     }
-    __syncthreads();
-    if (c < W) {
-      const int s3 = e[c] + e[c + 1] + e[c + 2];
-      const bool cur = s3 <= 1 && prev_sky;
-      prev_sky = cur;
-      if (!cur) md = fmin(xy[(size_t)row * W + c], md);
+#pragma unroll
+    for (int k = 0; k < SKY_RC; ++k) {
+      const int row = r0 + k;
+      if (row < H - 1) {                // uniform; no break, so the loop unrolls and nx stays in VGPRs
+        const double xp1 = nx[k];
+        int* eb = e[row & 1];
+        if (act) {
+          obf[(size_t)row * W + c] = x0 > md + 5 ? 1 : 0;
+          eb[c + 1] = (x0 != md) + (xm1 != md) + (xp1 != md);
+        }
+        __syncthreads();
+        if (act) {
+          const int s3 = eb[c] + eb[c + 1] + eb[c + 2];
+          const bool cur = s3 <= 1 && prev_sky;
+          prev_sky = cur;
+          if (!cur) md = fmin(x0, md);
+        }
+        xm1 = x0;
+        x0 = xp1;
+      }
     }
-    __syncthreads();
   }
-  if (c < W) {
-    obf[(size_t)(H - 1) * W + c] = xy[(size_t)(H - 1) * W + c] > md + 5 ? 1 : 0;
+  if (act) {
+    obf[(size_t)(H - 1) * W + c] = x0 > md + 5 ? 1 : 0;   // x0 = row H-1 here
     for (int row = 0; row < H; ++row) sky[(size_t)row * W + c] = 0;   // skyMask[:] = False (L304)
+  }
+}
+
+// the z-buffer words: nearest-depth bits and winner index start at all-ones
+__global__ __launch_bounds__(256) void proj_init_kernel(unsigned long long* __restrict__ dbest,
+                                                        unsigned int* __restrict__ ibest, size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    dbest[i] = ~0ull;
+    ibest[i] = ~0u;
   }
 }
 
@@ -154,10 +181,8 @@ hipError_t range_project(const double* pts, int N, int stride, int has_int, doub
   unsigned long long* dbest = reinterpret_cast<unsigned long long*>(ws);
   unsigned int* ibest = reinterpret_cast<unsigned int*>(dbest + n);
   double* xy = reinterpret_cast<double*>(reinterpret_cast<char*>(ibest) + ((n * 4 + 7) / 8) * 8);
-  hipError_t e = hipMemsetAsync(dbest, 0xff, n * 8, st);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(ibest, 0xff, n * 4, st);
-  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(proj_init_kernel, dim3((int)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0, st, dbest,
+                     ibest, n);
   const int grid = (int)std::min<size_t>(((size_t)N + 255) / 256, 4096);
   if (N > 0) {
     hipLaunchKernelGGL(proj_depth_kernel, dim3(grid), dim3(256), 0, st, pts, stride, N, g, dbest);
@@ -165,7 +190,8 @@ hipError_t range_project(const double* pts, int N, int stride, int has_int, doub
   }
   hipLaunchKernelGGL(proj_pixel_kernel, dim3((int)((n + 255) / 256)), dim3(256), 0, st, pts, stride, has_int, g, ibest,
                      depth, inten, xy, index);
-  hipLaunchKernelGGL(proj_sky_kernel, dim3(1), dim3(((W + 63) / 64) * 64), 0, st, xy, H, W, obf, sky);
+  if (obf)   // callers that only need the depth / intensity (a goal scan) skip the sequential scan
+    hipLaunchKernelGGL(proj_sky_kernel, dim3(1), dim3(((W + 63) / 64) * 64), 0, st, xy, H, W, obf, sky);
   return hipGetLastError();
 }
 
@@ -182,7 +208,7 @@ int sdp_range_project_workspace_size(int H, int W, size_t* bytes) {
 int sdp_range_project(const double* points, int N, int stride, int has_intensity, const double* origin, int H, int W,
                       double* depth, double* intensity, uint8_t* obfuscation, uint8_t* sky, int64_t* index, void* ws,
                       size_t ws_bytes, void* stream) {
-  if ((!points && N > 0) || N < 0 || !origin || !depth || !obfuscation || !sky || !ws)
+  if ((!points && N > 0) || N < 0 || !origin || !depth || (!obfuscation) != (!sky) || !ws)
     return sdp_fail("sdp_range_project: bad argument");
   if (ws_bytes < sdp::range_project_ws_bytes(H, W)) return sdp_fail("sdp_range_project: workspace too small");
   hipError_t e = sdp::range_project(points, N, stride, has_intensity, origin[0], origin[1], origin[2], H, W, depth,

@@ -93,19 +93,21 @@ class _KITTI360View:
         return self.length
 
     # ------------------------------------------------------------------ device steps
-    def _project(self, pts64, origin):
+    def _project(self, pts64, origin, masks=True):
+        """sdp_range_project; masks=False (a goal scan: only depth and intensity are used) skips
+        the sky / obfuscation scan."""
         H, W, dev = self.rowMax, self.colMax, self.device
         if self._ws is None:
             self._ws = _Workspace(H, W, dev)
         depth = torch.empty(H, W, dtype=torch.float64, device=dev)
         inten = torch.empty(H, W, dtype=torch.float64, device=dev)
-        obf = torch.empty(H, W, dtype=torch.uint8, device=dev)
-        sky = torch.empty(H, W, dtype=torch.uint8, device=dev)
+        obf = torch.empty(H, W, dtype=torch.uint8, device=dev) if masks else None
+        sky = torch.empty(H, W, dtype=torch.uint8, device=dev) if masks else None
         index = torch.empty(H, W, dtype=torch.int64, device=dev)
         o = np.ascontiguousarray(np.asarray(origin, dtype=np.float64).reshape(3))
         N = pts64.shape[0]
         _lib.check(_lib.lib().sdp_range_project(pts64.data_ptr() if N else None, N, 4, 1, o.ctypes.data, H, W,
-                                                depth.data_ptr(), inten.data_ptr(), obf.data_ptr(), sky.data_ptr(),
+                                                depth.data_ptr(), inten.data_ptr(), _lib.ptr(obf), _lib.ptr(sky),
                                                 index.data_ptr(), self._ws.ws.data_ptr(), self._ws.ws.numel(),
                                                 _lib.stream()), "range_project")
         return depth, inten, obf, sky, index
@@ -171,7 +173,7 @@ class _KITTI360View:
             origin = np.zeros(3) if self.variant == 0 else self.modifications[number_in_batch]
             ret_to_world, ret_from_world = goal_to_world, from_world
         depth, inten, obf, sky, index = self._project(view_pts, origin)
-        gdepth, ginten, _, _, _ = self._project(goal_pts, origin)
+        gdepth, ginten, _, _, _ = self._project(goal_pts, origin, masks=False)
         roll = int(np.random.randint(self.colMax))          # drawn on every item (8Batch:234)
         C = 2
         real = torch.empty(C, H, W, dtype=torch.float64, device=self.device)
