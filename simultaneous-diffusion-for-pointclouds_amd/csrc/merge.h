@@ -19,15 +19,18 @@ struct MergeArgs {
   const int32_t* refmask;  // [n_src][2][HW]
   const double* trig;      // cos_az[W], sin_az[W], cos_el[H], sin_el[H]
   double4* world;          // [n_src][HW] world point + source-valid flag
-  // accumulators, [nrep][n_out][cells]: source view vl scatters into replica vl % nrep, so a
-  // cell's atomics spread over nrep addresses (a 32-view megabatch otherwise serialises ~32
-  // atomics per cell); merge_reduce folds the replicas into replica 0 in a fixed order
+  // per-cell results [n_out][cells] (cells = big x W), written once per cell by merge_tile
   uint32_t* cnt;
   double* sumL;
   double* sumI;
   unsigned long long* minkey;
-  uint32_t* minidx;        // [n_out][cells]
-  int nrep;
+  uint32_t* minidx;
+  // binning of the (output view, source point) pairs by destination tile = (output view, big
+  // row): per-chunk tile counts [T][nchunk] -> exclusive offsets (tile-major), and the records
+  uint32_t* tcount;        // [T][nchunk], scanned in place
+  uint32_t* bsum;          // scan block totals
+  float4* rec;             // [pairs]: (code as 2 floats' bits, intensity, s << 10 | column)
+  int nchunk;
   float* newimg;           // [n_out][2][HW]
   uint8_t* maskimg;        // [n_out][HW]
   const uint32_t* absmax;  // max |x[:,0]| bits over all views
@@ -37,7 +40,6 @@ struct MergeArgs {
   float smod, allowance, cc, min_code;
 };
 
-int merge_replicas(int aB);
 size_t merge_ws_bytes(int n_src, int n_out, int H, int W);
 hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why);
 

@@ -8,8 +8,8 @@
 //     cnt (u32), sum of log-depth codes (f64), sum of intensities (f64),
 //     nearest code (u64 atomicMin on the f64 bits; codes are >= 0 so the order is the
 //     unsigned order), then the lowest source index among the nearest (second pass).
-// Large megabatches scatter into several replicas of the grids (by source view) that a
-// reduce pass folds, so no cell serialises one atomic per source view.
+// The accumulation bins the pairs by destination row so each cell is summed in LDS and
+// written once (global atomics run at the memory side, ≈10 G/s for scattered lanes).
 // A resolve pass turns a cell into the reference's controlled average (mean depth unless
 // it exceeds the nearest depth + allowance), applies the negative-depth flip/roll and crop
 // to the output view, and an apply pass adds cc * (-mask*(x - new)) on unknown pixels
@@ -98,67 +98,223 @@ __device__ __noinline__ Proj project(const MergeArgs& a, double4 w, int o) {
   return pr;
 }
 
-// ---------------------------------------------------------------- K1: accumulate
-__global__ __launch_bounds__(256) void merge_accum_kernel(MergeArgs a) {
-  const int HW = a.g.H * a.g.W;
+// ---------------------------------------------------------------- K1-K4: binned accumulation
+// Global atomics execute at the memory side at one chip-wide rate (≈10 G/s for lanes that hit
+// scattered addresses), and every pair needs four (count, two sums, nearest code): a 32-view
+// megabatch spent 3.8 ms of an 18.8-ms step there.  Instead the pairs are binned by
+// destination tile = (output view, big-grid row):
+//   K1 bin_count  : each chunk of pairs projects its points and counts them per tile (LDS);
+//   scan          : exclusive offsets over [tile][chunk] (tile-major);
+//   K3 bin_scatter: the chunks project again and write one 16-B record per pair into their
+//                   tile's range (LDS cursors);
+//   K4 segments   : workgroups take 4096 consecutive (so tile-sorted) records, sum them per
+//                   cell in LDS (ds atomics) and add each touched cell to the grids once, with
+//                   contiguous lanes; a second sweep finds the lowest source index among the
+//                   nearest.  (One workgroup per tile was 5.9 ms: the horizon rows hold most
+//                   records.)
+__device__ __forceinline__ void pair_of(const MergeArgs& a, size_t i, int HW, int& ol, int& s, int& o, int& m0) {
   const size_t per_out = (size_t)a.aB * HW;
-  const size_t n = (size_t)a.n_out * per_out;
-  const int cells = a.g.big * a.g.W;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int ol = i / per_out;
-    const int s = i % per_out;
-    const int o = a.o_begin + ol;
-    const int m0 = (o / a.aB) * a.aB;
-    const int vl = s / HW, p = s % HW;
-    const double4 w = a.world[(size_t)(m0 + vl) * HW + p];
-    const Proj pr = project(a, w, o);
+  ol = (int)(i / per_out);
+  s = (int)(i % per_out);
+  o = a.o_begin + ol;
+  m0 = (o / a.aB) * a.aB;
+}
+
+__global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_t per_chunk) {
+  extern __shared__ uint32_t hist[];
+  const int HW = a.g.H * a.g.W, T = a.n_out * a.g.big;
+  for (int t = threadIdx.x; t < T; t += 256) hist[t] = 0u;
+  __syncthreads();
+  const size_t n = (size_t)a.n_out * a.aB * HW;
+  const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += 256) {
+    int ol, s, o, m0;
+    pair_of(a, i, HW, ol, s, o, m0);
+    const Proj pr = project(a, a.world[(size_t)m0 * HW + s], o);
+    if (pr.cell >= 0) atomicAdd(&hist[ol * a.g.big + pr.cell / a.g.W], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += 256) a.tcount[(size_t)t * a.nchunk + blockIdx.x] = hist[t];
+}
+
+__global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, size_t per_chunk) {
+  extern __shared__ uint32_t cur[];
+  const int HW = a.g.H * a.g.W, T = a.n_out * a.g.big;
+  constexpr int SB = 2048;   // scan block (see scan kernels)
+  for (int t = threadIdx.x; t < T; t += 256) {
+    const size_t k = (size_t)t * a.nchunk + blockIdx.x;
+    cur[t] = a.tcount[k] + a.bsum[k / SB];
+  }
+  __syncthreads();
+  const size_t n = (size_t)a.n_out * a.aB * HW;
+  const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += 256) {
+    int ol, s, o, m0;
+    pair_of(a, i, HW, ol, s, o, m0);
+    const Proj pr = project(a, a.world[(size_t)m0 * HW + s], o);
     if (pr.cell < 0) continue;
-    const size_t ci = ((size_t)(vl % a.nrep) * a.n_out + ol) * cells + pr.cell;
-    atomicAdd(&a.cnt[ci], 1u);
-    atomicAdd(&a.sumL[ci], pr.code);
-    atomicAdd(&a.sumI[ci], (double)a.x[((size_t)(m0 + vl) * 2 + 1) * HW + p]);
-    atomicMin(&a.minkey[ci], (unsigned long long)__double_as_longlong(pr.code));
+    const int row = pr.cell / a.g.W, col = pr.cell % a.g.W;
+    const uint32_t pos = atomicAdd(&cur[ol * a.g.big + row], 1u);
+    const float inten = a.x[((size_t)m0 * 2 + 1) * HW + (size_t)(s / HW) * 2 * HW + (s % HW)];
+    const unsigned long long cb = (unsigned long long)__double_as_longlong(pr.code);
+    a.rec[pos] = make_float4(__uint_as_float((uint32_t)cb), __uint_as_float((uint32_t)(cb >> 32)), inten,
+                             __uint_as_float(((uint32_t)s << 10) | (uint32_t)col));
   }
 }
 
-// ---------------------------------------------------------------- K1b: fold the replicas
-__global__ __launch_bounds__(256) void merge_reduce_kernel(MergeArgs a) {
-  const size_t n = (size_t)a.n_out * a.g.big * a.g.W;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    uint32_t c = a.cnt[i];
-    double l = a.sumL[i], in = a.sumI[i];
-    unsigned long long mk = a.minkey[i];
-    for (int r = 1; r < a.nrep; ++r) {
-      const size_t j = (size_t)r * n + i;
-      c += a.cnt[j];
-      l = __dadd_rn(l, a.sumL[j]);
-      in = __dadd_rn(in, a.sumI[j]);
-      mk = a.minkey[j] < mk ? a.minkey[j] : mk;
+// exclusive scan of v[0..n) in blocks of 2048 (block totals -> bsum), then of the totals
+// (grand total -> bsum[nb]); consumers add bsum[k / 2048] to v[k]
+__global__ __launch_bounds__(256) void merge_scan_block_kernel(uint32_t* __restrict__ v, size_t n,
+                                                               uint32_t* __restrict__ bsum) {
+  __shared__ uint32_t sh[256];
+  const int tid = threadIdx.x;
+  const size_t base = blockIdx.x * 2048ull + tid * 8;
+  uint32_t x[8], t = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    x[k] = base + k < n ? v[base + k] : 0u;
+    t += x[k];
+  }
+  sh[tid] = t;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const uint32_t y = tid >= off ? sh[tid - off] : 0u;
+    __syncthreads();
+    sh[tid] += y;
+    __syncthreads();
+  }
+  uint32_t run = sh[tid] - t;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (base + k < n) v[base + k] = run;
+    run += x[k];
+  }
+  if (tid == 255) bsum[blockIdx.x] = sh[255];
+}
+
+__global__ __launch_bounds__(1024) void merge_scan_top_kernel(uint32_t* __restrict__ bsum, int nb) {
+  __shared__ uint32_t sh[1024];
+  const int tid = threadIdx.x, per = (nb + 1023) / 1024;
+  const int b0 = tid * per;
+  uint32_t t = 0;
+  for (int k = 0; k < per; ++k) t += b0 + k < nb ? bsum[b0 + k] : 0u;
+  sh[tid] = t;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {
+    const uint32_t y = tid >= off ? sh[tid - off] : 0u;
+    __syncthreads();
+    sh[tid] += y;
+    __syncthreads();
+  }
+  uint32_t run = sh[tid] - t;
+  for (int k = 0; k < per; ++k)
+    if (b0 + k < nb) {
+      const uint32_t x = bsum[b0 + k];
+      bsum[b0 + k] = run;
+      run += x;
     }
-    a.cnt[i] = c;
-    a.sumL[i] = l;
-    a.sumI[i] = in;
-    a.minkey[i] = mk;
+  if (tid == 1023) bsum[nb] = sh[1023];
+}
+
+// record range of tile t: [tile_off(t), tile_off(t + 1)), the last one ending at the total
+__device__ __forceinline__ uint32_t tile_off(const MergeArgs& a, int t, int T, int nb) {
+  if (t >= T) return a.bsum[nb];
+  const size_t k = (size_t)t * a.nchunk;
+  return a.tcount[k] + a.bsum[k / 2048];
+}
+// the tile whose range holds record j (largest t with tile_off(t) <= j)
+__device__ __forceinline__ int tile_of(const MergeArgs& a, uint32_t j, int T, int nb) {
+  int lo = 0, hi = T - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tile_off(a, mid, T, nb) <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// K4a: a workgroup sums MERGE_SEG consecutive records (tile-sorted) in LDS over the first two
+// tiles they touch (records of further tiles, a sparse stretch, go straight to global
+// atomics) and adds its cells to the grids: one atomic per touched cell, contiguous lanes.
+constexpr int MERGE_SEG = 4096;
+__global__ __launch_bounds__(256) void merge_seg_sum_kernel(MergeArgs a, int nb) {
+  __shared__ uint32_t scnt[2048];
+  __shared__ double ssl[2048], ssi[2048];
+  __shared__ unsigned long long smk[2048];
+  const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big, big = a.g.big;
+  const uint32_t total = a.bsum[nb];
+  const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
+  if (j0 >= total) return;
+  for (int c = tid; c < 2 * W; c += 256) {
+    scnt[c] = 0u;
+    ssl[c] = 0.0;
+    ssi[c] = 0.0;
+    smk[c] = ~0ull;
+  }
+  const int t0 = tile_of(a, j0, T, nb);
+  const uint32_t e1 = tile_off(a, t0 + 1, T, nb), e2 = tile_off(a, t0 + 2, T, nb);
+  __syncthreads();
+  for (uint32_t j = j0 + tid; j < j1; j += 256) {
+    const float4 r = a.rec[j];
+    const unsigned long long cb =
+        (unsigned long long)__float_as_uint(r.x) | ((unsigned long long)__float_as_uint(r.y) << 32);
+    const int col = __float_as_uint(r.w) & 1023u;
+    const double code = __longlong_as_double((long long)cb);
+    if (j < e2) {
+      const int c = (j < e1 ? 0 : W) + col;
+      atomicAdd(&scnt[c], 1u);
+      atomicAdd(&ssl[c], code);
+      atomicAdd(&ssi[c], (double)r.z);
+      atomicMin(&smk[c], cb);
+    } else {
+      const int t = tile_of(a, j, T, nb);
+      const size_t ci = ((size_t)(t / big) * big + t % big) * W + col;
+      atomicAdd(&a.cnt[ci], 1u);
+      atomicAdd(&a.sumL[ci], code);
+      atomicAdd(&a.sumI[ci], (double)r.z);
+      atomicMin(&a.minkey[ci], cb);
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < 2 * W; c += 256) {
+    const int t = t0 + c / W;
+    if (t >= T || scnt[c] == 0u) continue;
+    const size_t ci = (size_t)t * W + c % W;     // tile t = ol * big + row -> cell row-major per view
+    atomicAdd(&a.cnt[ci], scnt[c]);
+    atomicAdd(&a.sumL[ci], ssl[c]);
+    atomicAdd(&a.sumI[ci], ssi[c]);
+    atomicMin(&a.minkey[ci], smk[c]);
   }
 }
 
-// ---------------------------------------------------------------- K2: lowest index among nearest
-__global__ __launch_bounds__(256) void merge_minidx_kernel(MergeArgs a) {
-  const int HW = a.g.H * a.g.W;
-  const size_t per_out = (size_t)a.aB * HW;
-  const size_t n = (size_t)a.n_out * per_out;
-  const int cells = a.g.big * a.g.W;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int ol = i / per_out;
-    const int s = i % per_out;
-    const int o = a.o_begin + ol;
-    const int m0 = (o / a.aB) * a.aB;
-    const int vl = s / HW, p = s % HW;
-    const double4 w = a.world[(size_t)(m0 + vl) * HW + p];
-    const Proj pr = project(a, w, o);
-    if (pr.cell < 0) continue;
-    const size_t ci = (size_t)ol * cells + pr.cell;
-    if ((unsigned long long)__double_as_longlong(pr.code) == a.minkey[ci]) atomicMin(&a.minidx[ci], (uint32_t)s);
+// K4b: the lowest source index among the records whose code equals the cell's nearest code
+__global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a, int nb) {
+  __shared__ uint32_t sidx[2048];
+  const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big;
+  const uint32_t total = a.bsum[nb];
+  const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
+  if (j0 >= total) return;
+  for (int c = tid; c < 2 * W; c += 256) sidx[c] = 0xffffffffu;
+  const int t0 = tile_of(a, j0, T, nb);
+  const uint32_t e1 = tile_off(a, t0 + 1, T, nb), e2 = tile_off(a, t0 + 2, T, nb);
+  __syncthreads();
+  for (uint32_t j = j0 + tid; j < j1; j += 256) {
+    const float4 r = a.rec[j];
+    const unsigned long long cb =
+        (unsigned long long)__float_as_uint(r.x) | ((unsigned long long)__float_as_uint(r.y) << 32);
+    const uint32_t w = __float_as_uint(r.w);
+    const int col = w & 1023u;
+    const int t = j < e2 ? (j < e1 ? t0 : t0 + 1) : tile_of(a, j, T, nb);
+    const size_t ci = (size_t)t * W + col;
+    if (cb != a.minkey[ci]) continue;
+    if (j < e2) atomicMin(&sidx[(j < e1 ? 0 : W) + col], w >> 10);
+    else atomicMin(&a.minidx[ci], w >> 10);
+  }
+  __syncthreads();
+  for (int c = tid; c < 2 * W; c += 256) {
+    const int t = t0 + c / W;
+    if (t >= T || sidx[c] == 0xffffffffu) continue;
+    atomicMin(&a.minidx[(size_t)t * W + c % W], sidx[c]);
   }
 }
 
@@ -235,21 +391,27 @@ __global__ __launch_bounds__(256) void merge_apply_kernel(MergeArgs a) {
 
 static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 256 * 16); }
 
-// replicas of the accumulator grids: 1 up to a 7-view megabatch, then one per 2 views, at most 8
-// (measured on one MI355X, 4 output views: a 32-view megabatch costs 25.4 ms/step with one
-// grid, 18.6 ms with 8 replicas, 19.1 ms with 16)
-int merge_replicas(int aB) { return aB < 8 ? 1 : (aB / 2 > 8 ? 8 : aB / 2); }
+// pair chunks of the binning passes: ~1024 (4 per CU), at least 2048 pairs each
+static int merge_chunks(size_t npair) { return (int)std::max<size_t>(1, std::min<size_t>(1024, (npair + 2047) / 2048)); }
 
 size_t merge_ws_bytes(int n_src, int n_out, int H, int W) {
   const int big = (int)((25 * 2) * (long)H / 28);
   const size_t cells = (size_t)big * W;
-  const int R = merge_replicas(n_src);                // aB <= n_src
+  const size_t npair = (size_t)n_out * n_src * H * W;       // aB <= n_src
+  const size_t T = (size_t)n_out * big, nt = T * merge_chunks(npair);
   size_t b = 0;
-  b += (size_t)n_src * H * W * sizeof(double4);      // world
-  b += (size_t)R * n_out * cells * (4 + 8 + 8 + 8) + 4 * 256;  // cnt, sumL, sumI, minkey (replicated)
-  b += (size_t)n_out * cells * 4;                    // minidx
-  b += (size_t)n_out * 2 * H * W * 4;                // newimg (internal)
-  b += (size_t)n_out * H * W;                        // maskimg
+  auto add = [&](size_t x) { b += (x + 255) & ~size_t(255); };
+  add((size_t)n_src * H * W * sizeof(double4));             // world
+  add(cells * n_out * 4);                                    // cnt
+  add(cells * n_out * 8);                                    // sumL
+  add(cells * n_out * 8);                                    // sumI
+  add(cells * n_out * 8);                                    // minkey
+  add(cells * n_out * 4);                                    // minidx
+  add(nt * 4);                                               // tcount
+  add(((nt + 2047) / 2048 + 1) * 4);                         // bsum
+  add(npair * 16);                                           // records
+  add((size_t)n_out * 2 * H * W * 4);                        // newimg (internal)
+  add((size_t)n_out * H * W);                                // maskimg
   return b + 1024;
 }
 
@@ -258,30 +420,46 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   const size_t cells = (size_t)a.g.big * W;
   if (ws_bytes < merge_ws_bytes(a.n_src, a.n_out, H, W)) { *why = "merge: workspace too small"; return hipErrorInvalidValue; }
   if (a.n_src % a.aB || a.o_begin < 0 || a.o_begin + a.n_out > a.n_src) { *why = "merge: bad view ranges"; return hipErrorInvalidValue; }
-  if (W % 2) { *why = "merge: W must be even"; return hipErrorInvalidValue; }
+  if (W % 2 || W > 1024) { *why = "merge: W must be even and <= 1024"; return hipErrorInvalidValue; }
+  if ((size_t)a.aB * H * W > (1u << 22)) { *why = "merge: aB*H*W must be < 2^22 (record packing)"; return hipErrorInvalidValue; }
+  const size_t npair = (size_t)a.n_out * a.aB * H * W, nout = (size_t)a.n_out * H * W, nw = (size_t)a.n_src * H * W;
+  const int T = a.n_out * a.g.big;
+  a.nchunk = merge_chunks(npair);
+  const size_t nt = (size_t)T * a.nchunk;
+  const int nb = (int)((nt + 2047) / 2048);
+  if (nb > 8 * 1024) { *why = "merge: too many tiles x chunks"; return hipErrorInvalidValue; }
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) & ~size_t(255); return q; };
-  a.world = reinterpret_cast<double4*>(take((size_t)a.n_src * H * W * sizeof(double4)));
-  a.nrep = merge_replicas(a.aB);
-  const size_t rc = (size_t)a.nrep * a.n_out * cells;
-  char* acc0 = p;
-  a.cnt = reinterpret_cast<uint32_t*>(take(rc * 4));
-  a.sumL = reinterpret_cast<double*>(take(rc * 8));
-  a.sumI = reinterpret_cast<double*>(take(rc * 8));
-  char* ff0 = p;
-  a.minkey = reinterpret_cast<unsigned long long*>(take(rc * 8));
-  a.minidx = reinterpret_cast<uint32_t*>(take((size_t)a.n_out * cells * 4));
-  char* ff1 = p;
+  a.world = reinterpret_cast<double4*>(take(nw * sizeof(double4)));
+  a.cnt = reinterpret_cast<uint32_t*>(take(cells * a.n_out * 4));
+  a.sumL = reinterpret_cast<double*>(take(cells * a.n_out * 8));
+  a.sumI = reinterpret_cast<double*>(take(cells * a.n_out * 8));
+  a.minkey = reinterpret_cast<unsigned long long*>(take(cells * a.n_out * 8));
+  a.minidx = reinterpret_cast<uint32_t*>(take(cells * a.n_out * 4));
+  a.tcount = reinterpret_cast<uint32_t*>(take(nt * 4));
+  a.bsum = reinterpret_cast<uint32_t*>(take(((nt + 2047) / 2048 + 1) * 4));
+  a.rec = reinterpret_cast<float4*>(take(npair * 16));
   a.newimg = new_out ? new_out : reinterpret_cast<float*>(take((size_t)a.n_out * 2 * H * W * 4));
   a.maskimg = reinterpret_cast<uint8_t*>(take((size_t)a.n_out * H * W));
+  const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
+  const size_t lds = (size_t)T * 4;
+  if (lds > 64 * 1024) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
+  // grids: sums / counts 0, nearest code and index all-ones (cnt..sumI and minkey..minidx are
+  // contiguous in the workspace)
   hipError_t e;
-  if ((e = hipMemsetAsync(acc0, 0, ff0 - acc0, st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(ff0, 0xFF, ff1 - ff0, st)) != hipSuccess) return e;
-  const size_t nw = (size_t)a.n_src * H * W, npair = (size_t)a.n_out * a.aB * H * W, nout = (size_t)a.n_out * H * W;
+  if ((e = hipMemsetAsync(a.cnt, 0, reinterpret_cast<char*>(a.minkey) - reinterpret_cast<char*>(a.cnt), st)) != hipSuccess)
+    return e;
+  if ((e = hipMemsetAsync(a.minkey, 0xFF, reinterpret_cast<char*>(a.tcount) - reinterpret_cast<char*>(a.minkey), st)) !=
+      hipSuccess)
+    return e;
   hipLaunchKernelGGL(merge_world_kernel, dim3(grid_for(nw)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(merge_accum_kernel, dim3(grid_for(npair)), dim3(256), 0, st, a);
-  if (a.nrep > 1) hipLaunchKernelGGL(merge_reduce_kernel, dim3(grid_for((size_t)a.n_out * cells)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(merge_minidx_kernel, dim3(grid_for(npair)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(merge_bin_count_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
+  hipLaunchKernelGGL(merge_scan_block_kernel, dim3(nb), dim3(256), 0, st, a.tcount, nt, a.bsum);
+  hipLaunchKernelGGL(merge_scan_top_kernel, dim3(1), dim3(1024), 0, st, a.bsum, nb);
+  hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
+  const int nseg = (int)((npair + MERGE_SEG - 1) / MERGE_SEG);   // upper bound: records <= pairs
+  hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), 0, st, a, nb);
+  hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), 0, st, a, nb);
   hipLaunchKernelGGL(merge_resolve_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_apply_kernel, dim3(grid_for(2 * nout)), dim3(256), 0, st, a);
   return hipGetLastError();
