@@ -134,7 +134,9 @@ typedef struct sdp_merge_params {
   float cc;               /* correlation coefficient                                       */
 } sdp_merge_params;
 
-int sdp_merge_workspace_size(int n_src, int n_out, int H, int W, size_t* bytes);
+int sdp_merge_workspace_size(int n_src, int n_out, int H, int W, size_t* bytes);   /* any aB <= n_src */
+/* the same for megabatches of exactly aB views (the pair records scale with n_out * aB * H * W) */
+int sdp_merge_workspace_bytes(int n_src, int aB, int n_out, int H, int W, size_t* bytes);
 /*
  * x_all   : [n_src,2,H,W] current images of every source view (device, float32)
  * toWorld : [n_src,4,4] float64 (POSES) ; fromWorld : [n_src,4,4] float64 (POSES)

@@ -40,7 +40,7 @@ struct MergeArgs {
   float smod, allowance, cc, min_code;
 };
 
-size_t merge_ws_bytes(int n_src, int n_out, int H, int W);
+size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W);   // aB <= n_src
 hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why);
 
 }  // namespace sdp

@@ -394,10 +394,10 @@ static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 25
 // pair chunks of the binning passes: ~1024 (4 per CU), at least 2048 pairs each
 static int merge_chunks(size_t npair) { return (int)std::max<size_t>(1, std::min<size_t>(1024, (npair + 2047) / 2048)); }
 
-size_t merge_ws_bytes(int n_src, int n_out, int H, int W) {
+size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   const int big = (int)((25 * 2) * (long)H / 28);
   const size_t cells = (size_t)big * W;
-  const size_t npair = (size_t)n_out * n_src * H * W;       // aB <= n_src
+  const size_t npair = (size_t)n_out * aB * H * W;
   const size_t T = (size_t)n_out * big, nt = T * merge_chunks(npair);
   size_t b = 0;
   auto add = [&](size_t x) { b += (x + 255) & ~size_t(255); };
@@ -418,7 +418,7 @@ size_t merge_ws_bytes(int n_src, int n_out, int H, int W) {
 hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why) {
   const int H = a.g.H, W = a.g.W;
   const size_t cells = (size_t)a.g.big * W;
-  if (ws_bytes < merge_ws_bytes(a.n_src, a.n_out, H, W)) { *why = "merge: workspace too small"; return hipErrorInvalidValue; }
+  if (ws_bytes < merge_ws_bytes(a.n_src, a.aB, a.n_out, H, W)) { *why = "merge: workspace too small"; return hipErrorInvalidValue; }
   if (a.n_src % a.aB || a.o_begin < 0 || a.o_begin + a.n_out > a.n_src) { *why = "merge: bad view ranges"; return hipErrorInvalidValue; }
   if (W % 2 || W > 1024) { *why = "merge: W must be even and <= 1024"; return hipErrorInvalidValue; }
   if ((size_t)a.aB * H * W > (1u << 22)) { *why = "merge: aB*H*W must be < 2^22 (record packing)"; return hipErrorInvalidValue; }

@@ -42,7 +42,14 @@ extern "C" {
 
 int sdp_merge_workspace_size(int n_src, int n_out, int H, int W, size_t* bytes) {
   if (!bytes || n_src <= 0 || n_out <= 0 || H <= 0 || W <= 0) return sdp_fail("sdp_merge_workspace_size: bad argument");
-  *bytes = trig_bytes(H, W) + merge_ws_bytes(n_src, n_out, H, W);
+  *bytes = trig_bytes(H, W) + merge_ws_bytes(n_src, n_src, n_out, H, W);   // any megabatch size
+  return 0;
+}
+
+int sdp_merge_workspace_bytes(int n_src, int aB, int n_out, int H, int W, size_t* bytes) {
+  if (!bytes || n_src <= 0 || aB <= 0 || aB > n_src || n_out <= 0 || H <= 0 || W <= 0)
+    return sdp_fail("sdp_merge_workspace_bytes: bad argument");
+  *bytes = trig_bytes(H, W) + merge_ws_bytes(n_src, aB, n_out, H, W);
   return 0;
 }
 

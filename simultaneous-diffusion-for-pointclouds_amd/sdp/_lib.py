@@ -62,6 +62,7 @@ _SIGS = {
     "sdp_langevin_step": (I, [P, P, P, P, P, U64, U64, F, F, F, I, I, I, I, P, P, P]),
     "sdp_axpy_step": (I, [P, P, F, P, P, P, F, I, P]),
     "sdp_merge_workspace_size": (I, [I, I, I, I, C.POINTER(SZ)]),
+    "sdp_merge_workspace_bytes": (I, [I, I, I, I, I, C.POINTER(SZ)]),
     "sdp_consistency_merge": (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, C.POINTER(MergeParams), P, P, P, SZ, P]),
 }
 

@@ -48,7 +48,7 @@ class Merger:
         self.sky = torch.as_tensor(sky).reshape(B, H, W).to(dev).to(torch.uint8).contiguous()
         self.refmask = torch.as_tensor(refmask).to(dev, torch.int32).contiguous()
         n = _lib.SZ()
-        _lib.check(_lib.lib().sdp_merge_workspace_size(B, self.n_out, H, W, _lib.C.byref(n)), "merge_ws")
+        _lib.check(_lib.lib().sdp_merge_workspace_bytes(B, aB, self.n_out, H, W, _lib.C.byref(n)), "merge_ws")
         self.ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
 
     def __call__(self, x: torch.Tensor, sigma, setting: int, allowance: float, cc: float, absmax: torch.Tensor,
