@@ -20,6 +20,14 @@ hipError_t axpy_step(float* x, const float* g, float a, const float* lik, const 
                      size_t n, hipStream_t st);
 
 // ---- training (DSM backward; train_aux.hip, wgrad.hip, conv_bwd.hip)
+// one conv's weights for pack_weights_multi: output slots [begin, begin + Cout*Cin*NT)
+struct PackDesc {
+  const float* w;
+  uint32_t* out;
+  int Cout, Cin, NT, dgrad;
+  size_t begin;
+};
+hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st);
 hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k, int mode, int dgrad, hipStream_t st);
 hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
                          int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,

@@ -69,6 +69,10 @@ struct sdp_net {
       if (!in_arena) (void)hipFree(kv.second);
     }
     dev.clear();
+    if (pack_dev) (void)hipFree(pack_dev);
+    pack_dev = nullptr;
+    pack_dev_n = 0;
+    pack_host.clear();
     if (arena_owned && arena) (void)hipFree(arena);
     arena = nullptr;
     arena_owned = false;
@@ -99,8 +103,14 @@ struct sdp_net {
     auto it = host.find(k);
     return it != host.end() && it->second.shape.size() == 4 && k != "begin_conv.weight" && k != "end_conv.weight";
   }
-  // (re)build the fragment-ordered weights from the fp32 parameters on the device
+  // (re)build the fragment-ordered weights from the fp32 parameters on the device: one
+  // launch over every conv (a descriptor table, re-uploaded when a parameter moves)
+  std::vector<sdp::PackDesc> pack_host;
+  sdp::PackDesc* pack_dev = nullptr;
+  size_t pack_dev_n = 0, pack_total = 0;
   void repack(hipStream_t st) {
+    std::vector<sdp::PackDesc> d;
+    size_t total = 0;
     for (auto& kv : host) {
       if (!is_conv_w(kv.first)) continue;
       const auto& s = kv.second.shape;
@@ -108,15 +118,31 @@ struct sdp_net {
       for (int dg = 0; dg < (train_packs ? 2 : 1); ++dg) {
         const std::string fk = kv.first + (dg ? "#dfrag" : "#frag");
         if (!dev.count(fk)) {
-          void* d = nullptr;
-          sdp::chk(hipMalloc(&d, bytes), "hipMalloc");
-          dev[fk] = d;
+          void* p = nullptr;
+          sdp::chk(hipMalloc(&p, bytes), "hipMalloc");
+          dev[fk] = p;
         }
-        sdp::chk(sdp::pack_weights(P(kv.first), reinterpret_cast<uint32_t*>(dev[fk]), (int)s[0], (int)s[1], (int)s[2],
-                                   mode, dg, st),
-                 "pack_weights");
+        d.push_back(sdp::PackDesc{P(kv.first), reinterpret_cast<uint32_t*>(dev[fk]), (int)s[0], (int)s[1],
+                                  (int)(s[2] * s[3]), dg, total});
+        total += kv.second.data.size();
       }
     }
+    const bool same = d.size() == pack_host.size() &&
+                      std::equal(d.begin(), d.end(), pack_host.begin(), [](const sdp::PackDesc& x, const sdp::PackDesc& y) {
+                        return x.w == y.w && x.out == y.out && x.begin == y.begin && x.dgrad == y.dgrad;
+                      });
+    if (!same) {
+      if (pack_dev_n < d.size()) {
+        if (pack_dev) sdp::chk(hipFree(pack_dev), "hipFree");
+        sdp::chk(hipMalloc(&pack_dev, d.size() * sizeof(sdp::PackDesc)), "hipMalloc");
+        pack_dev_n = d.size();
+      }
+      pack_host = d;
+      sdp::chk(hipMemcpyAsync(pack_dev, pack_host.data(), d.size() * sizeof(sdp::PackDesc), hipMemcpyHostToDevice, st),
+               "hipMemcpyAsync");
+      pack_total = total;
+    }
+    sdp::chk(sdp::pack_weights_multi(pack_dev, (int)pack_host.size(), pack_total, mode, st), "pack_weights_multi");
   }
 };
 

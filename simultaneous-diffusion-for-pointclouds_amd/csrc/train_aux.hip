@@ -29,40 +29,54 @@ SDP_DEV float wsum(float v) {
 // BF16 : 16-bit element (s, hl, j) of lane l, s in {0,1}, hl in {hi, lo}, j < 8:
 //        ci' = chunk*32 + 16*s + 8*(l>>5) + j ; hi = bf16(w), lo = bf16(w - hi)
 // dgrad: W'[o][i][tap] = W[i][o][k*k-1-tap]   (Cout' = Cin, Cin' = Cout)
+SDP_DEV uint32_t pack_slot(const float* __restrict__ w, int Cout, int Cin, int NT, int mode, int dgrad, size_t i) {
+  const int Co = dgrad ? Cin : Cout;
+  const int NB = Co / 32;
+  const int slot = i & 15;
+  size_t r = i >> 4;
+  const int lane = r & 63;
+  r >>= 6;
+  const int nb = r % NB;
+  r /= NB;
+  const int tap = r % NT;
+  const int ch = r / NT;
+  const int co = nb * 32 + (lane & 31), h = lane >> 5;
+  auto wv = [&](int ci) -> float {
+    return dgrad ? w[((size_t)ci * Cin + co) * NT + (NT - 1 - tap)] : w[((size_t)co * Cin + ci) * NT + tap];
+  };
+  if (mode == MODE_F32) return __float_as_uint(wv(ch * 32 + 16 * h + slot));
+  const int s = slot >> 3, hl = (slot >> 2) & 1, j0 = (slot & 3) * 2;
+  uint32_t pk = 0;
+  for (int e = 0; e < 2; ++e) {
+    const float f = wv(ch * 32 + 16 * s + 8 * h + j0 + e);
+    const __bf16 hi = (__bf16)f;
+    const __bf16 q = hl ? (__bf16)(f - (float)hi) : hi;
+    pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
+  }
+  return pk;
+}
+
 __global__ void pack_weights_kernel(const float* __restrict__ w, uint32_t* __restrict__ out, int Cout, int Cin, int NT,
                                     int mode, int dgrad) {
-  const int Co = dgrad ? Cin : Cout, Ci = dgrad ? Cout : Cin;
-  const int NB = Co / 32;
-  const size_t n = (size_t)Co * Ci * NT;    // output 32-bit slots
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int slot = i & 15;
-    size_t r = i >> 4;
-    const int lane = r & 63;
-    r >>= 6;
-    const int nb = r % NB;
-    r /= NB;
-    const int tap = r % NT;
-    const int ch = r / NT;
-    const int co = nb * 32 + (lane & 31), h = lane >> 5;
-    auto wv = [&](int ci) -> float {
-      return dgrad ? w[((size_t)ci * Cin + co) * NT + (NT - 1 - tap)] : w[((size_t)co * Cin + ci) * NT + tap];
-    };
-    uint32_t v;
-    if (mode == MODE_F32) {
-      v = __float_as_uint(wv(ch * 32 + 16 * h + slot));
-    } else {
-      const int s = slot >> 3, hl = (slot >> 2) & 1, j0 = (slot & 3) * 2;
-      uint32_t pk = 0;
-      for (int e = 0; e < 2; ++e) {
-        const float f = wv(ch * 32 + 16 * s + 8 * h + j0 + e);
-        const __bf16 hi = (__bf16)f;
-        const __bf16 q = hl ? (__bf16)(f - (float)hi) : hi;
-        pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
-      }
-      v = pk;
-    }
-    out[i] = v;
-  }
+  const size_t n = (size_t)Cout * Cin * NT;    // output 32-bit slots
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = pack_slot(w, Cout, Cin, NT, mode, dgrad, i);
+}
+
+// every conv of the network in one launch (the re-pack after each optimizer step):
+// blockIdx.y picks the conv, the x blocks stride over its slots
+__global__ void pack_weights_multi_kernel(const PackDesc* __restrict__ d, int mode) {
+  const PackDesc e = d[blockIdx.y];
+  const size_t n = (size_t)e.Cout * e.Cin * e.NT;
+  for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x)
+    e.out[j] = pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
+}
+
+hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st) {
+  if (nd <= 0) return hipSuccess;
+  (void)total;
+  hipLaunchKernelGGL(pack_weights_multi_kernel, dim3(64, nd), dim3(256), 0, st, d, mode);
+  return hipGetLastError();
 }
 
 hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k, int mode, int dgrad, hipStream_t st) {
