@@ -175,9 +175,9 @@ def test_merge_large_megabatch_vs_oracle():
 
 
 @pytest.mark.parametrize("aB,W", [(16, 256), (32, 128)])
-def test_merge_replicated_accumulators_vs_oracle(aB, W):
-    """Megabatches of 16 / 32 views (4 / 8 accumulator replicas folded by merge_reduce; the
-    BASELINE config-4 megabatch is 32) against the oracle restatement."""
+def test_merge_large_megabatch_vs_oracle(aB, W):
+    """Megabatches of 16 / 32 views (the BASELINE config-4 megabatch is 32): the binned
+    accumulation sums many 4096-record segments per destination row, against the oracle."""
     case = GI.merge_case(f"big{aB}", aB, 64, W)
     new, xc = _gpu_merge(case, aB, 0.7, 5, 10, 0.01)
     on, ox = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
