@@ -184,37 +184,39 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
 // ---------------------------------------------------------------- IN++ finalize
 // stats [B][T][C] of float2 (tile mean, tile M2) with `cnt` values per tile -> ss [B][C] of
 // float2 (scale, shift) such that IN++(x) = x*scale + shift.  Two launches:
-//   inpp_moments : one 256-thread block per (image, 64 channels), 4 tile groups; Chan merge
+//   inpp_moments : one 1024-thread block per (image, 64 channels), 16 tile groups; Chan merge
 //                  of the equal-count partials in float64 -> (mean, biased var) per (b, c)
 //   inpp_ss      : one block per image over its C channels: m = mean_c(mean), v = unbiased
 //                  var_c(mean) (normalization.py:164-166), then the affine of every channel
-__global__ __launch_bounds__(256) void inpp_moments_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
-                                                           double2* __restrict__ mv) {
-  __shared__ double red[256];
-  const int cb = C / 64;
-  const int b = blockIdx.x / cb, c = (blockIdx.x % cb) * 64 + (threadIdx.x & 63), g = threadIdx.x >> 6;
+constexpr int INPP_G = 16;   // tile groups (one wave each) per inpp_moments block of 64 channels
+__global__ __launch_bounds__(64 * INPP_G) void inpp_moments_kernel(const float2* __restrict__ stats, int T, float cnt,
+                                                                   int C, double2* __restrict__ mv) {
+  __shared__ double red[64 * INPP_G];
+  const int cb = C / 64, l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int b = blockIdx.x / cb, c = (blockIdx.x % cb) * 64 + l;
   const float2* st = stats + (size_t)b * T * C + c;
+  auto block_sum = [&](double v) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < INPP_G; ++k) s += red[k * 64 + l];   // fixed order: deterministic
+    __syncthreads();
+    return s;
+  };
   double sm = 0.0;
 #pragma unroll 4
-  for (int t = g; t < T; t += 4) sm += st[(size_t)t * C].x;
-  red[threadIdx.x] = sm;
-  __syncthreads();
-  const double mean = (red[threadIdx.x & 63] + red[64 + (threadIdx.x & 63)] + red[128 + (threadIdx.x & 63)] +
-                       red[192 + (threadIdx.x & 63)]) / T;
-  __syncthreads();
+  for (int t = g; t < T; t += INPP_G) sm += st[(size_t)t * C].x;
+  const double mean = block_sum(sm) / T;
   double m2 = 0.0;
 #pragma unroll 4
-  for (int t = g; t < T; t += 4) {
+  for (int t = g; t < T; t += INPP_G) {
     const float2 v = st[(size_t)t * C];
     const double dm = (double)v.x - mean;
     m2 += (double)v.y + dm * dm * cnt;
   }
-  red[threadIdx.x] = m2;
-  __syncthreads();
-  if (g == 0) {
-    m2 = red[threadIdx.x] + red[64 + threadIdx.x] + red[128 + threadIdx.x] + red[192 + threadIdx.x];
-    mv[(size_t)b * C + c] = make_double2(mean, m2 / ((double)T * cnt));   // biased (nn.InstanceNorm2d)
-  }
+  m2 = block_sum(m2);
+  if (g == 0) mv[(size_t)b * C + c] = make_double2(mean, m2 / ((double)T * cnt));   // biased (nn.InstanceNorm2d)
 }
 
 __global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict__ mv, int C,
@@ -333,7 +335,7 @@ hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, con
                          const float* beta, float* ss, hipStream_t st, float* nst, void* scratch) {
   if (C % 64 || C > 1024 || (C & (C - 1))) return hipErrorInvalidValue;
   double2* mv = reinterpret_cast<double2*>(scratch);
-  hipLaunchKernelGGL(inpp_moments_kernel, dim3(B * (C / 64)), dim3(256), 0, st, reinterpret_cast<const float2*>(stats), T,
+  hipLaunchKernelGGL(inpp_moments_kernel, dim3(B * (C / 64)), dim3(64 * INPP_G), 0, st, reinterpret_cast<const float2*>(stats), T,
                      cnt, C, mv);
   hipLaunchKernelGGL(inpp_ss_kernel, dim3(B), dim3(C), 0, st, mv, C, alpha, gamma, beta, reinterpret_cast<float2*>(ss),
                      reinterpret_cast<float4*>(nst));
