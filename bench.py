@@ -28,6 +28,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -46,6 +47,11 @@ PROJECT_METRIC = ("KITTI-360 views rendered/sec (pose chain + view and goal poin
                   "post-processing) at 64×1024, 1/2/4/8 MI355X")
 HBM_PEAK = 8000.0             # GB/s, MI355X_MICROARCH.md
 PEAK = {"fp32": 157.3, "fp32x3": 2500.0 / 3, "bf16": 2500.0}  # dense MFMA TFLOP/s in algorithmic fp32 FLOPs
+DTYPE_NOTE = {
+    "fp32x3": "fp32 I/O, accumulation and non-conv ops; conv products as 3 bf16 MFMA passes of the hi/lo split "
+              "(hi*hi + hi*lo + lo*hi, ~2^-17 relative product error; parity tol 1e-4 of max|out|)",
+    "fp32": "exact fp32 products (v_mfma_f32_32x32x2_f32), fp32 everywhere",
+    "bf16": "bf16 conv operands, fp32 accumulation and non-conv ops"}
 FWD_FLOP = 1.2663e12          # score-net forward FLOPs per 64x1024 image
 # Inpainting.yml (HDVMine_Circle.yml) data.modifications + 2 more origins: 8 aux views (config 3)
 CIRCLE9 = [[0, 0, 0], [5, -5, 0], [-5, -5, 0], [0, 5, 0], [-10, 10, 0], [10, 10, 0], [-10, 0, 0], [10, 0, 0],
@@ -54,7 +60,8 @@ CIRCLE9 = [[0, 0, 0], [5, -5, 0], [-5, -5, 0], [0, 5, 0], [-10, 10, 0], [10, 10,
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node; without torchrun's env, N > 1 spawns N ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["line", "allforone", "train", "project"], default="line")
@@ -65,6 +72,10 @@ def parse():
                          "fixed) -- one rank's per-step work of BASELINE config 4 (32) without the all-gather")
     ap.add_argument("--precision", choices=["fp32x3", "fp32", "bf16"], default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the world it saw")
+    ap.add_argument("--no-fp32-line", action="store_true",
+                    help="skip the exact-fp32 (v_mfma_f32_32x32x2_f32) companion measurement of the line workload")
     ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
     if a.views is None:
@@ -125,22 +136,27 @@ def cpu_baseline_train(H, W, threads):
                       f"(torch CPU fp32), {dt:.2f} s"}
 
 
-def pmc_traffic(precision, V):
-    """HBM bytes per launch of the dominant conv class from the committed PMC passes
-    (tools/pmc_traffic.sh -> profiles/r01_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
-    correction) + TCC_EA0_WRREQ bytes, averaged over that kernel's launches at this grid)."""
-    mode = {"fp32": 0, "fp32x3": 1, "bf16": 2}[precision]
-    name = f"void sdp::conv_mfma_kernel<{mode}, 1, 64, 3, false, false, true>(sdp::ConvArgs)"
-    grid = V * (32 * 512 // 128) * 256
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
+
+
+def pmc_traffic(precision, V, cls):
+    """HBM bytes per launch of the dominant conv class, read from the committed PMC passes
+    (tools/pmc_traffic.sh -> profiles/r02_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
+    correction) + TCC_EA0_WRREQ bytes per launch of that kernel at this grid).  PMC counters cannot
+    be read inside this process, so the value is tagged with the file's source hash: when it does
+    not match the current csrc tree the traffic is reported as null (stale), never as current."""
     try:
-        with open(os.path.join(REPO, "profiles", "r01_traffic.json")) as f:
-            rows = json.load(f)
+        with open(TRAFFIC_FILE) as f:
+            doc = json.load(f)
     except OSError:
-        return None
-    for r in rows:
-        if r["kernel"] == name and r["grid"] == grid and "hbm_bytes" in r:
-            return round(r["hbm_bytes"])
-    return None
+        return None, None
+    from sdp import _build
+    if doc.get("source_hash") != _build.source_hash():
+        return None, f"stale: {os.path.basename(TRAFFIC_FILE)} was measured on another csrc tree"
+    for r in doc.get("rows", []):
+        if r.get("precision") == precision and r.get("views") == V and r.get("class") == cls:
+            return round(r["hbm_bytes"]), f"{os.path.basename(TRAFFIC_FILE)} (PMC, source {doc['source_hash'][:12]})"
+    return None, None
 
 
 # ----------------------------------------------------------------------------- timing harness
@@ -207,50 +223,68 @@ def run_sampling(args, rank, N, dist, dev):
     grad = torch.empty_like(x)
     L = _lib.lib()
     st = _lib.stream()
-    offset = [0]
+    per_view4 = 2 * H * W // 4
+    offset = [o_begin * per_view4]            # Philox counters of the whole megabatch (sdp/sampling.py)
 
     def step(i):
         c = 2 + (i % (len(sig) - 2))          # levels >= minStepToShare: the merge always runs
         s = np.float32(6.2e-6) * (sig[c] / sig[-1]) ** 2
         ns = np.float32(np.sqrt(np.float32(s * np.float32(2))))
-        net(x, labels[c], out=grad)
+        net_box[0](x, labels[c], out=grad)
         absmax.zero_()
         _lib.check(L.sdp_langevin_step(x.data_ptr(), grad.data_ptr(), ref.data_ptr(), mask.data_ptr(), None,
-                                       1234 + rank, offset[0], float(s), float(ns), 1.0, 1, V, 2, H * W,
-                                       lik.data_ptr(), absmax.data_ptr(), st), "langevin")
-        offset[0] += x.numel() // 4
+                                       1234 + (rank if args.mode == "megabatch" else 0), offset[0], float(s),
+                                       float(ns), 1.0, 1, V, 2, H * W, lik.data_ptr(), absmax.data_ptr(), st),
+                   "langevin")
+        offset[0] += n_src * per_view4
         if dist:
             if args.mode == "viewsplit":
                 torch.distributed.all_gather_into_tensor(x_all, x)     # cross-view consistency gather
             torch.distributed.all_reduce(absmax, op=torch.distributed.ReduceOp.MAX)
         merger(x_all, sig[c], setting, 10, 0.01, absmax)
 
-    net.profile(True)
-    net.profile_read()
-    for i in range(args.warmup):
-        step(i)
-    net.profile_read()                                  # drop the warmup launches
-    dt = timed(step, argparse.Namespace(warmup=0, steps=args.steps), dist, dev)
-    prof = net.profile_read()
-    net.profile(False)
+    def measure(prec, steps, warmup):
+        """Time `steps` steps with the score net at conv arithmetic `prec`; return (dt, roofline)."""
+        net_box[0] = net if prec == args.precision else ScoreNet(H=H, W=W, precision=prec).load_synthetic()
+        cur = net_box[0]
+        cur.profile(True)
+        cur.profile_read()
+        for i in range(warmup):
+            step(i)
+        cur.profile_read()                                  # drop the warmup launches
+        dt = timed(step, argparse.Namespace(warmup=0, steps=steps), dist, dev)
+        prof = cur.profile_read()
+        cur.profile(False)
+        if rank == 0:
+            for k, (n_, ms_, fl_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+                print(f"[conv {prec}] {k:34s} launches {n_:5d} avg {ms_ / n_ * 1e3:8.1f} us  "
+                      f"{fl_ / (ms_ / n_ / 1e3) / 1e12:7.1f} TF/s", file=sys.stderr)
+        cls, (n, ms, fl) = max(prof.items(), key=lambda kv: kv[1][1])
+        avg_s = ms / n / 1e3
+        achieved = fl / avg_s / 1e12
+        conv_ms = sum(v[1] for v in prof.values()) / steps
+        traffic, tsrc = pmc_traffic(prec, V, cls) if args.workload == "line" else (None, None)
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[prec], 1),
+                "unit": "TFLOP/s", "frac": round(achieved / PEAK[prec], 4),
+                "traffic": traffic, "traffic_source": tsrc,
+                "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if prec == "bf16" else 4),
+                "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
+                "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3)}
+        return dt, roof
+
+    net_box = [net]
+    dt, roof = measure(args.precision, args.steps, args.warmup)
+    exact = None
+    if args.workload == "line" and args.precision != "fp32" and not args.no_fp32_line:
+        k = min(args.steps, 5)
+        dt32, roof32 = measure("fp32", k, 1)
+        exact = {"value": round(N * V * k / dt32, 3), "ms_per_step": round(dt32 / k * 1e3, 3), "steps": k,
+                 "dtype": "fp32", "roofline": roof32,
+                 "note": "same step with exact-fp32 conv products (v_mfma_f32_32x32x2_f32)"}
     assert torch.isfinite(x_all).all(), "non-finite images"
     if rank != 0:
         return None
-    for k, (n_, ms_, fl_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
-        print(f"[conv] {k:34s} launches {n_:5d} avg {ms_ / n_ * 1e3:8.1f} us  {fl_ / (ms_ / n_ / 1e3) / 1e12:7.1f} TF/s",
-              file=sys.stderr)
     value = N * V * args.steps / dt
-    cls, (n, ms, fl) = max(prof.items(), key=lambda kv: kv[1][1])
-    avg_s = ms / n / 1e3
-    achieved = fl / avg_s / 1e12
-    conv_ms = sum(v[1] for v in prof.values()) / args.steps
-    roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[args.precision], 1),
-            "unit": "TFLOP/s", "frac": round(achieved / PEAK[args.precision], 4),
-            "traffic": pmc_traffic(args.precision, V) if args.workload == "line" else None,
-            "traffic_unit": "bytes/launch (PMC, profiles/r01_traffic.json)",
-            "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if args.precision == "bf16" else 4),
-            "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
-            "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3)}
     cpu = None
     if N == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(V, H, W, args.cpu_threads, args.workload)
@@ -262,12 +296,13 @@ def run_sampling(args, rank, N, dist, dev):
               "64x1024x2 range images")
     return {"metric": METRIC, "value": round(value, 3), "unit": "image-steps/s", "n_gpus": N,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "dtype_note": DTYPE_NOTE[args.precision],
             "data": "synthetic (procedural Line.yml-style scene, random-init NCSN_LiDAR_small weights)",
             "config": {"workload": wl + (" (megabatch emulated on one GPU)" if args.megabatch_views else ""),
                        "views_per_gpu": V, "megabatch_views": aB, "mode": args.mode,
                        "conv_arithmetic": args.precision, "parallelism": f"views{N}"},
-            "roofline": roof, "cpu_baseline": cpu}
+            "roofline": roof, "cpu_baseline": cpu, "fp32_exact": exact}
 
 
 def run_train(args, rank, N, dist, dev):
@@ -442,12 +477,50 @@ def run_project(args, rank, N, dist, dev):
             "roofline": roof, "cpu_baseline": cpu}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launcher_cmd(gpus, argv, port):
+    """The torchrun command that runs this bench as one process per GPU (RCCL over xGMI)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus or 1) > 1:
+        # `bench.py --gpus N` without a launcher: spawn N ranks (this parent never touches the GPU)
+        if not args.dry_run:
+            from sdp import _build
+            _build.ensure_built()
+        sys.exit(subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], _free_port())))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    if args.dry_run:
+        if dist:
+            torch.distributed.init_process_group("gloo")
+            t = torch.tensor([rank], dtype=torch.int64)
+            torch.distributed.all_reduce(t)
+            if rank == 0:
+                print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": torch.distributed.get_world_size(),
+                                  "rank_sum": int(t.item())}))
+            torch.distributed.destroy_process_group()
+        else:
+            print(json.dumps({"dry_run": True, "n_gpus": 1, "world_size": 1, "rank_sum": 0}))
+        return
+    from sdp import _build
+    _build.ensure_built()          # a fresh checkout has no libsdp.so (git-ignored): build before any GPU call
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist:
@@ -459,6 +532,9 @@ def main():
     else:
         line = run_sampling(args, rank, world, dist, dev)
     if line is not None:
+        if dist:
+            line["world_size"] = torch.distributed.get_world_size()
+            line["backend"] = torch.distributed.get_backend()
         print(json.dumps(line))
     if dist:
         torch.distributed.destroy_process_group()

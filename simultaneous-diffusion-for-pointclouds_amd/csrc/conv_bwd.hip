@@ -15,7 +15,6 @@ static hipError_t launch_dgrad_t(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS>;
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
-  a.tiles_per_wg = 1;   // the LDS-staged backward epilogue overwrites the pipeline's buffers
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
   return hipGetLastError();

@@ -95,24 +95,15 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c;
   // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so give each XCD a
   // contiguous range of tiles -- vertically adjacent tiles share their halo rows in its L2
-  // A workgroup runs a.tiles_per_wg consecutive tiles of one image (forward launches of big
-  // grids): the K pipeline runs on across the tile boundary -- the next tile's first two
-  // chunks are landed and transformed during the current tile's last two -- so only the
-  // first tile pays the pipeline fill.
-  const int nwg = gridDim.x, tpw = a.tiles_per_wg > 1 ? a.tiles_per_wg : 1;
-  const int t0 = ((nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3)) * tpw;
-  const int b = t0 / a.tiles_per_img;
-  int tile, ph_r, ph_c, sr0, sc0;
-  auto decode = [&](int tl, int& ph_r_, int& ph_c_, int& sr0_, int& sc0_) __attribute__((always_inline)) {
-    const int ph = tl / tiles_rc;
-    tl -= ph * tiles_rc;
-    ph_r_ = ph / d;
-    ph_c_ = ph - (ph / d) * d;
-    sr0_ = (tl / tiles_c) * T::TR;
-    sc0_ = (tl % tiles_c) * TC;
-  };
-  tile = t0 - b * a.tiles_per_img;
-  decode(tile, ph_r, ph_c, sr0, sc0);
+  const int nwg = gridDim.x;
+  int t = (nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3);
+  const int b = t / a.tiles_per_img;
+  const int tile = t - b * a.tiles_per_img;
+  t = tile;
+  const int ph = t / tiles_rc;
+  t -= ph * tiles_rc;
+  const int ph_r = ph / d, ph_c = ph - (ph / d) * d;
+  const int sr0 = (t / tiles_c) * T::TR, sc0 = (t % tiles_c) * TC;
   const int n0 = blockIdx.y * T::NTILE;
   const int wrow0 = wm * T::RW;                    // wave's first tile row
 
@@ -171,45 +162,36 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   // reads zeros instead of running off the tensor
   const __amdgpu_buffer_rsrc_t irs =
       __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, a.H * a.W * Cin * 4, 0x00020000);
-  int uoff[NU], uoffn[NU];   // this tile's / the next tile's (tiles_per_wg > 1) unit offsets
-  unsigned uvalid = 0, uvalidn = 0;
-  auto unit_offsets = [&](int sr0_, int sc0_, int ph_r_, int ph_c_, int* uo, unsigned& uv) __attribute__((always_inline)) {
-    uv = 0;
-    static_for<0, NU>([&](auto kc) {
-      constexpr int k = decltype(kc)::value;
-      int u = tid + k * 256;
-      bool valid = u < T::NPIX * 8;
-      u = valid ? u : 0;
-      const int pix = u >> 3, cv = u & 7;
-      const int pr = pix / T::PC, pc = pix - pr * T::PC;
-      int sr = sr0_ - T::HALO + pr, sc = sc0_ - T::HALO + pc;
-      if (a.circular) {
-        sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
-        sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
-      } else {
-        valid = valid && sr >= 0 && sr < Hs && sc >= 0 && sc < Ws;
-        sr = min(max(sr, 0), Hs - 1);
-        sc = min(max(sc, 0), Ws - 1);
-      }
-      const int y = sr * d + ph_r_, x = sc * d + ph_c_;
-      uo[k] = ((y * a.W + x) * Cin + cv * 4) * 4;   // bytes, < 2^31 for every admitted shape
-      uv |= (valid ? 1u : 0u) << k;
-    });
-  };
-  unit_offsets(sr0, sc0, ph_r, ph_c, uoff, uvalid);
-  bool has_next = false;   // (uniform) the chunks past this tile's last belong to the next tile
-  // chunk index of the pipeline's look-ahead: past the last chunk it is the next tile's (or
-  // a dead re-load of the last chunk)
-  auto ahead = [&](int c) __attribute__((always_inline)) { return c < nchunks ? c : (has_next ? c - nchunks : nchunks - 1); };
+  int uoff[NU];
+  unsigned uvalid = 0;
+  static_for<0, NU>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    int u = tid + k * 256;
+    bool valid = u < T::NPIX * 8;
+    u = valid ? u : 0;
+    const int pix = u >> 3, cv = u & 7;
+    const int pr = pix / T::PC, pc = pix - pr * T::PC;
+    int sr = sr0 - T::HALO + pr, sc = sc0 - T::HALO + pc;
+    if (a.circular) {
+      sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
+      sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
+    } else {
+      valid = valid && sr >= 0 && sr < Hs && sc >= 0 && sc < Ws;
+      sr = min(max(sr, 0), Hs - 1);
+      sc = min(max(sc, 0), Ws - 1);
+    }
+    const int y = sr * d + ph_r, x = sc * d + ph_c;
+    uoff[k] = ((y * a.W + x) * Cin + cv * 4) * 4;   // bytes, < 2^31 for every admitted shape
+    uvalid |= (valid ? 1u : 0u) << k;
+  });
   // LDS-DMA of staging unit k: lane i of a wave lands 16 B at the wave-uniform base + 16*i
   auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     if constexpr (SDP_KO & 1) return;
     const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
-    const bool nx = has_next && chunk >= nchunks;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
-        nx ? uoffn[k] : uoff[k], (nx ? chunk - nchunks : chunk) * 128, 0, 0);
+        uoff[k], chunk * 128, 0, 0);
   };
   // transform staging unit k of raw into patch buffer PB
   // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
@@ -322,7 +304,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
       constexpr int CUR = NBUF == 3 ? tap % 3 : (tap + P) & 1;
       constexpr int NXT = NBUF == 3 ? (tap + DIST) % 3 : (tap + 1 + P) & 1;
       if constexpr (tap + DIST < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + DIST);
-      else load_b(std::integral_constant<int, NXT>{}, ahead(chunk + 1), tap + DIST - NT);
+      else load_b(std::integral_constant<int, NXT>{}, min(chunk + 1, nchunks - 1), tap + DIST - NT);
       __builtin_amdgcn_sched_barrier(0);
       // next chunk's transform on taps [0, XT), then the chunk after next's DMA on the rest
       // this tap's share of the next chunk's transform (units k with k % XT == tap)
@@ -337,7 +319,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         });
       };
       auto dmas = [&]() __attribute__((always_inline)) {
-        if constexpr (tap == NT - 1) load_ss(ahead(chunk + 2));
+        if constexpr (tap == NT - 1) load_ss(min(chunk + 2, nchunks - 1));
         static_for<0, NU>([&](auto kc) {
           constexpr int dt = NT > XT ? XT : 0;   // all at the first free tap: the longest flight
           if constexpr (dt == tap) load_unit(kc, chunk + 2);
@@ -426,13 +408,6 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
 #endif
   };
   static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
-  int n_ph_r = 0, n_ph_c = 0, n_sr0 = 0, n_sc0 = 0;   // the next tile (tiles_per_wg > 1)
-  for (int it = 0;; ++it) {
-  has_next = it + 1 < tpw;
-  if (has_next) {
-    decode(tile + 1, n_ph_r, n_ph_c, n_sr0, n_sc0);
-    unit_offsets(n_sr0, n_sc0, n_ph_r, n_ph_c, uoffn, uvalidn);
-  }
   for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
     do_chunk(std::integral_constant<int, 0>{}, chunk);
     do_chunk(std::integral_constant<int, 1>{}, chunk + 1);
@@ -745,19 +720,6 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
       });
     }
   }
-  if (!has_next) break;
-  // on to the next tile: its first chunk is transformed in patch[0], its second in flight
-  tile += 1;
-  ph_r = n_ph_r; ph_c = n_ph_c; sr0 = n_sr0; sc0 = n_sc0;
-  static_for<0, NU>([&](auto kc) { uoff[decltype(kc)::value] = uoffn[decltype(kc)::value]; });
-  uvalid = uvalidn;
-  static_for<0, 4>([&](auto i) {
-    static_for<0, 2>([&](auto j) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    });
-  });
-  }   // tiles of this workgroup
 #ifdef SDP_TIMING
   SDP_T(4);
   if (tid == 0) {

@@ -70,9 +70,12 @@ _lib = None
 
 
 def lib():
-    """Load libsdp.so once; raise loudly if it is absent (no fallback path exists)."""
+    """Load libsdp.so once, building it first if it is missing or stale (sdp/_build.py). A build
+    failure raises with the compiler's output; there is no fallback path."""
     global _lib
     if _lib is None:
+        from . import _build
+        _build.ensure_built()
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libsdp.so not found at {LIB_PATH}: build it with `python __graft_entry__.py build` "
                                "(or `make -C simultaneous-diffusion-for-pointclouds_amd/csrc`)")

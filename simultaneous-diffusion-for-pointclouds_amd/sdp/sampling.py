@@ -70,7 +70,11 @@ class _Stepper:
         self.absmax = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.noise_fn = noise_fn
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
-        self.offset = 0
+        # Philox counters are per 4 elements of the WHOLE megabatch: a rank holding views
+        # [own0, own0+B) draws exactly the noise the single-process run draws for those views
+        self.per_view4 = self.C * self.H * self.W // 4
+        self.offset = own0 * self.per_view4
+        self.offset_stride = n_all * self.per_view4
         self._labels = {}
 
     def labels(self, c):
@@ -89,7 +93,7 @@ class _Stepper:
         self.absmax.zero_()
         self.ops.langevin(self.x, grad, self.ref, self.mask, noise, self.seed, self.offset, step_size, nscale,
                           grad_ref, nan_to_num, self.lik, self.absmax)
-        self.offset += self.x.numel() // 4
+        self.offset += self.offset_stride
 
     def denoise(self, grad, sigma_last, grad_ref):
         grad = grad.to(self.dev, torch.float32).contiguous()

@@ -15,6 +15,7 @@ import torch
 import torch.multiprocessing as mp
 
 from oracle import golden_inputs as GI
+from oracle import philox_ref
 from oracle import sampling_ref as S
 
 B_ALL, H, W = 4, 64, 128
@@ -44,6 +45,8 @@ class OracleMerger:
 class OracleOps:
     def langevin(self, x, grad, ref, mask, noise, seed, offset, step, nscale, grad_ref, nan_to_num, lik, absmax):
         g = S.nan_to_num(grad.numpy()) if nan_to_num else grad.numpy()
+        if noise is None:   # the kernel's Philox stream (seed, counter = offset + element/4)
+            noise = torch.from_numpy(philox_ref.normal(seed, offset, x.numel()).reshape(x.shape))
         lk = (-mask.numpy()).astype(np.float32) * (x.numpy() - ref.numpy())
         v = (((x.numpy() + np.float32(step) * g) + np.float32(grad_ref) * lk) + noise.numpy() * np.float32(nscale))
         x.copy_(torch.from_numpy(v.astype(np.float32)))
@@ -71,7 +74,7 @@ def _inputs():
     return case, x0
 
 
-def _run(rank, world, port, out_dir):
+def _run(rank, world, port, out_dir, philox=False):
     from sdp.sampling import anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti as samp
     if world > 1:
         torch.distributed.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
@@ -91,9 +94,9 @@ def _run(rank, world, port, out_dir):
         t(x0[sl].copy()), t(case["ref"][sl].copy()), t(case["mask"][sl].copy()), t(case["sky"][sl].copy()), None, 1, 5,
         10, fake_score, SIGMAS, t(case["fromWorld"]), t(case["toWorld"]), B_ALL, n_steps_each=2, step_lr=6.2e-6,
         existMask=t(case["exist"]), denoise=True, verbose=False, grad_ref=1, correlation_coefficient=0.01,
-        noise_fn=noise_fn, view_shard=(rank, world) if world > 1 else None, all_refer_mask=t(case["mask"]),
+        noise_fn=None if philox else noise_fn, view_shard=(rank, world) if world > 1 else None, all_refer_mask=t(case["mask"]),
         all_sky=t(case["sky"]), ops=OracleOps())
-    np.save(os.path.join(out_dir, f"w{world}_r{rank}.npy"), np.stack([im.numpy() for im in images]))
+    np.save(os.path.join(out_dir, f"w{world}_r{rank}{'_p' if philox else ''}.npy"), np.stack([im.numpy() for im in images]))
     if world > 1:
         torch.distributed.destroy_process_group()
 
@@ -106,11 +109,15 @@ def _free_port():
     return p
 
 
-def test_view_sharded_sampler_matches_single_process(tmp_path):
-    _run(0, 1, 0, str(tmp_path))
-    mp.spawn(_run, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
-    single = np.load(tmp_path / "w1_r0.npy")                       # [n_images, B_ALL, 2, H, W]
-    shard = np.concatenate([np.load(tmp_path / f"w2_r{r}.npy") for r in range(2)], axis=1)
+@pytest.mark.parametrize("philox", [False, True], ids=["injected_noise", "philox_noise"])
+def test_view_sharded_sampler_matches_single_process(tmp_path, philox):
+    """philox_noise: no noise_fn, so each rank draws the kernel's own counter-based stream; the
+    sharded run must draw the single-process noise for its views (counter offset = first view)."""
+    _run(0, 1, 0, str(tmp_path), philox)
+    mp.spawn(_run, args=(2, _free_port(), str(tmp_path), philox), nprocs=2, join=True)
+    sfx = "_p" if philox else ""
+    single = np.load(tmp_path / f"w1_r0{sfx}.npy")                 # [n_images, B_ALL, 2, H, W]
+    shard = np.concatenate([np.load(tmp_path / f"w2_r{r}{sfx}.npy") for r in range(2)], axis=1)
     assert single.shape == shard.shape
     np.testing.assert_array_equal(shard, single)
     assert np.abs(single[-1] - GI.scorenet_input("dist", B_ALL, H, W)).max() > 1e-3   # the sampler did move x

@@ -105,6 +105,31 @@ def test_philox_noise_statistics():
     v = x.cpu().numpy().reshape(-1)
     assert abs(v.mean()) < 0.01 and abs(v.std() - 1) < 0.01
     assert len(np.unique(v)) > 0.99 * n
+    # the stream itself: Philox4x32-10 + Box-Muller restated in numpy (oracle/philox_ref.py);
+    # device __logf/__sincosf vs numpy float32 log/sin/cos
+    from oracle import philox_ref
+    want = philox_ref.normal(1234, 0, n)
+    assert np.abs(v - want).max() <= 2e-5 * np.abs(want).max()
+
+
+def test_philox_view_shard_draws_the_single_process_stream():
+    """A rank holding views [2, 4) of a 4-view megabatch (counter offset 2 views) draws exactly
+    the noise the single-process call applies to those views (sdp/sampling.py _Stepper)."""
+    from sdp import _lib
+    HW = 64 * 1024
+
+    def run(B, offset):
+        x = torch.zeros(B, 2, HW, device=DEV)
+        z = torch.zeros_like(x)
+        m = torch.zeros(B, 2, HW, dtype=torch.int32, device=DEV)
+        _lib.check(_lib.lib().sdp_langevin_step(x.data_ptr(), z.data_ptr(), z.data_ptr(), m.data_ptr(), None, 77,
+                                                offset, 0.0, 1.0, 1.0, 1, B, 2, HW, None, None, _lib.stream()))
+        return x.cpu().numpy()
+
+    per_view4 = 2 * HW // 4
+    full = run(4, 3 * 4 * per_view4)            # step 3 of the single-process run
+    part = run(2, 3 * 4 * per_view4 + 2 * per_view4)
+    np.testing.assert_array_equal(part, full[2:])
 
 
 def _after_update(case):
@@ -164,7 +189,7 @@ def test_merge_too_high_disables_correction():
     np.testing.assert_array_equal(xc, _after_update(case))
 
 
-def test_merge_large_megabatch_vs_oracle():
+def test_merge_megabatch8_w512_vs_oracle():
     """aB=8 (more views than any golden) against the oracle restatement."""
     case = GI.merge_case("big8", 8, 64, 512)
     new, xc = _gpu_merge(case, 8, 0.7, 5, 10, 0.01)
