@@ -213,6 +213,38 @@ def gen_allforone():
         save(f"merge_{tag}.npz", new=imgs[0].numpy(), x=imgs[1].numpy())
 
 
+# Inpainting.yml (HDVMine_Circle.yml:73) origins + 2 more: the target + 8 aux views of BASELINE config 3
+CIRCLE9 = CIRCLE_MODS + [[10, 0, 0], [0, -10, 0]]
+BIG_VIEWS = [0, 17, 31]          # output views kept from the 32-view megabatch (each depends on all 32)
+
+
+def gen_allforone9():
+    """Config 3 geometry: B=aB=9 origin-offset merge, setting 7 (64x256)."""
+    models = _ref_imports()
+
+    def zero(x, y):
+        return torch.zeros_like(x)
+
+    case = GI.merge_case("a_b9_s05_set7", 9, 64, 256)
+    with torch.no_grad(), _NoiseFeed("merge"):
+        imgs, _, _ = models.anneal_Langevin_dynamics_inpainting_simultaneous_basic(
+            torch.from_numpy(case["x"]), torch.from_numpy(case["ref"]), torch.from_numpy(case["mask"]),
+            torch.from_numpy(case["sky"]), None, 0, 7, zero, np.array([0.5], np.float32),
+            torch.from_numpy(np.array(CIRCLE9)), 9, n_steps_each=1, step_lr=0.0,
+            existMask=torch.from_numpy(case["exist"]), denoise=False, verbose=False, grad_ref=1,
+            correlation_coefficient=0.01)
+    save("merge_a_b9_s05_set7.npz", new=imgs[0].numpy(), x=imgs[1].numpy())
+
+
+def gen_big():
+    """Config 4 geometry: ONE 32-view megabatch at the full 64x1024 (kitti poses, setting 5);
+    only BIG_VIEWS of the outputs are stored (3 MB instead of 33 MB)."""
+    models = _ref_imports()
+    case = GI.merge_case("k_b32a32_full", 32, 64, 1024)
+    new, xf = _kitti_merge(models, case, 32, 0.5)
+    save("merge_k_b32a32_full.npz", views=np.array(BIG_VIEWS), new=new[BIG_VIEWS], x=xf[BIG_VIEWS])
+
+
 def gen_config1():
     """Config 1: baseline sampler, B=1, sigmas[:1], 5 steps + denoise, injected noise (64x256)."""
     models = _ref_imports()
@@ -287,9 +319,9 @@ def gen_projection():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     what = sys.argv[1:] or ["exist", "scorenet", "ops", "langevin", "merge", "allforone", "config1", "e2e", "dsm",
-                            "projection"]
+                            "projection", "allforone9", "big"]
     _ref_imports()
     for w in what:
         {"exist": gen_exist, "scorenet": gen_scorenet, "ops": gen_ops, "langevin": gen_langevin,
          "merge": gen_merge, "allforone": gen_allforone, "config1": gen_config1, "e2e": gen_kitti_e2e,
-         "dsm": gen_dsm, "projection": gen_projection}[w]()
+         "dsm": gen_dsm, "projection": gen_projection, "allforone9": gen_allforone9, "big": gen_big}[w]()

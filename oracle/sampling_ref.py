@@ -136,11 +136,12 @@ def _apply(x, new, maskimg, sky, refmask, too_high, cc):
 
 
 def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5, allowance=10, cc=0.01,
-                absmax=None):
+                absmax=None, views=None):
     """One consistency merge of the pose-matrix sampler (KITTISampling.py:160-490).
 
     x f32 [B,2,H,W] (after the Langevin update); returns (newImages f32, x corrected f32).
     absmax: max|x[:,0]| over every view of the step when x holds only some of them.
+    views: compute only these output views (the others come back unmerged) -- large megabatches.
     """
     B, _, H, W = x.shape
     g = merge_geometry(H, W)
@@ -159,7 +160,7 @@ def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5
     ex = exist[:aB].reshape(-1)
     new = np.zeros_like(x)
     maskimg = np.zeros((B, H, W), bool)
-    for o in range(B):
+    for o in (range(B) if views is None else views):
         m0 = (o // aB) * aB
         src = Pw[m0:m0 + aB]                                 # [aB,4,HW]
         q = np.einsum("ij,vjn->vin", fromWorld[o], src)[:, :3].transpose(1, 0, 2).reshape(3, -1)
@@ -189,7 +190,7 @@ def allforone_origins(mods) -> np.ndarray:
     return ((o / den).astype(np.float32) * F32(10)).astype(np.float32)
 
 
-def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01):
+def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01, views=None):
     """One merge of the origin-offset sampler (models/__init__.py:263-579)."""
     B, _, H, W = x.shape
     g = merge_geometry(H, W)
@@ -206,7 +207,7 @@ def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01)
     allowance = 5 if setting >= 8 else 10
     new = np.zeros_like(x)
     maskimg = np.zeros((B, H, W), bool)
-    for o in range(B):
+    for o in (range(B) if views is None else views):
         m0 = (o // aB) * aB
         r = rd[m0:m0 + aB]
         px = (r * caz * cel + org[:, 0, None, None]).reshape(-1)

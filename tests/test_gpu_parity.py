@@ -183,6 +183,28 @@ def test_allforone_merge_matches_reference_golden(tag, setting):
     assert _close_frac(_final_dc(xc, case), f["x"]) <= 1e-4
 
 
+def test_allforone9_merge_matches_reference_golden():
+    """BASELINE config 3 geometry: target + 8 aux origins in one megabatch, setting 7."""
+    from oracle.gen_golden import CIRCLE9
+    from sdp.merge import allforone_origins
+    case = GI.merge_case("a_b9_s05_set7", 9, 64, 256)
+    f = _g("merge_a_b9_s05_set7.npz")
+    new, xc = _gpu_merge(case, 9, 0.5, 7, 10, 0.01, origins=allforone_origins(CIRCLE9))
+    assert _close_frac(new, f["new"]) <= 1e-4
+    assert _close_frac(_final_dc(xc, case), f["x"]) <= 1e-4
+
+
+def test_megabatch32_full_width_matches_reference_golden():
+    """BASELINE config 4 geometry: one 32-view megabatch at the full 64x1024 (views 0/17/31 stored)."""
+    case = GI.merge_case("k_b32a32_full", 32, 64, 1024)
+    f = _g("merge_k_b32a32_full.npz")
+    v = list(f["views"])
+    new, xc = _gpu_merge(case, 32, 0.5, 5, 10, 0.01)
+    assert _close_frac(new[v], f["new"]) <= 1e-4
+    assert _close_frac(_final_dc(xc, case)[v], f["x"]) <= 1e-4
+    assert np.mean((new[v] != 0) != (f["new"] != 0)) <= 1e-4
+
+
 def test_merge_too_high_disables_correction():
     case = GI.merge_case("k_b4a4_s05", 4, 64, 256)
     _, xc = _gpu_merge(case, 4, 0.5, 5, 10, 0.01, too_high=9.0)   # 9*6/1 > 50
