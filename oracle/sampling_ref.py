@@ -190,14 +190,15 @@ def allforone_origins(mods) -> np.ndarray:
     return ((o / den).astype(np.float32) * F32(10)).astype(np.float32)
 
 
-def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01, views=None):
-    """One merge of the origin-offset sampler (models/__init__.py:263-579)."""
+def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01, views=None, absmax=None):
+    """One merge of the origin-offset sampler (models/__init__.py:263-579).  absmax: as kitti_merge."""
     B, _, H, W = x.shape
     g = merge_geometry(H, W)
     smod = sigma_mod_of(sigma)
     x0 = x[:, 0]
     isneg = x0 < 0
-    too_high = bool(F32(F32(np.abs(x0).max()) * F32(6)) / F32(smod) > 50)
+    m = F32(np.abs(x0).max()) if absmax is None else F32(absmax)
+    too_high = bool(F32(m * F32(6)) / F32(smod) > 50)
     rd = real_distance(x0, smod).astype(np.float64)
     org = allforone_origins(mods).astype(np.float64)[:aB]       # [aB,3]
     caz, saz = np.cos(g["az"])[None, None, :], np.sin(g["az"])[None, None, :]

@@ -28,7 +28,7 @@ template <int MODE>
 static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
 #ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
   if (wm == 2) return launch_t<MODE, 2, 32, 3, false, true>(a, st);
-  return launch_t<MODE, 1, 64, 3, false, true>(a, st);
+  return tc == 64 ? launch_t<MODE, 1, 64, 3, false, true>(a, st) : launch_t<MODE, 1, 32, 3, false, true>(a, st);
 #else
   return a.pro_mode == PRO_NONE ? launch_elu<MODE, false>(a, ks, pool, wm, tc, st)
                                 : launch_elu<MODE, true>(a, ks, pool, wm, tc, st);
@@ -49,6 +49,9 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   const int wm = (a.Cout % 256 == 0) ? 1 : 2;
 #endif
   int tc = (wm == 2) ? 32 : ((Ws % 64 == 0) ? 64 : 32);
+#ifdef SDP_CONV_BENCH_ONLY   // SDP_TC=32|64 forces the tile width of the WM=1 shape
+  if (wm == 1 && getenv("SDP_TC")) tc = atoi(getenv("SDP_TC"));
+#endif
   if (ks == 1 || pool) tc = 64;
   const int tr = wm * 128 / tc;
   if (Ws % tc || Hs % tr) { *why = "conv: sub-grid not divisible by the pixel tile"; return hipErrorInvalidValue; }

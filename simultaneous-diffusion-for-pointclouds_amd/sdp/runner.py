@@ -18,6 +18,16 @@ Data: with ``args.kitti_root`` the views come from the KITTI-360 datasets of sdp
 (rendered on the GPU) in the order of the reference's MySampler over the pose file
 (kitti:494-515); otherwise from the procedural scene of ``sdp.synthetic`` (same 9-tuple
 contract, kitti360_im_8Batch.py:304).
+
+Multi-GPU (the reference's DataParallel, kitti:481): under torchrun (one process per GPU,
+torch.distributed initialised by main.py) every batch's megabatches are split into contiguous
+blocks, one per rank; each rank samples its block (tooHigh stays global through the samplers'
+4-byte all_reduce(MAX) over the active ranks, and each view draws the noise it would draw in a
+single-process run), the sampled images are gathered to rank 0, and rank 0 writes the files --
+the same files, bit for bit, as one process would.
+
+``train()`` is the kitti runner's DSM training loop (kitti:83-348; identical in
+ncsn_runner_AllForOne.py:88-353) on libsdp, data parallel over ranks (see ``train``).
 """
 from __future__ import annotations
 
@@ -29,6 +39,7 @@ import numpy as np
 import torch
 
 from . import kitti360, synthetic
+from .weights import synthetic_state_dict
 from .imgutil import make_grid, save_image
 from .sampling import (anneal_Langevin_dynamics_inpainting,
                        anneal_Langevin_dynamics_inpainting_simultaneous_basic,
@@ -64,6 +75,21 @@ def synthetic_batch(batch_index, B, aB, H, W, seed=1234):
             cat["fromWorld"].clone(), save_num)
 
 
+def shard_megabatches(n_mega, rank, world):
+    """[m0, m1): the contiguous block of megabatches rank `rank` samples (the first
+    n_mega % world ranks take one more; ranks past n_mega get none)."""
+    base, extra = divmod(n_mega, world)
+    m0 = rank * base + min(rank, extra)
+    return m0, m0 + base + (1 if rank < extra else 0)
+
+
+def _dist():
+    d = torch.distributed
+    if d.is_available() and d.is_initialized():
+        return d.get_rank(), d.get_world_size()
+    return 0, 1
+
+
 def _first_views(t, n_mega, aB, k):
     """Keep the first k views of every megabatch (the reference's reshape-and-slice, kitti:720-739)."""
     shp = t.shape
@@ -71,8 +97,10 @@ def _first_views(t, n_mega, aB, k):
 
 
 class Runner:
-    def __init__(self, args, config):
+    def __init__(self, args, config, score=None, ops=None):
+        """score / ops: injected score network and device ops (tests); default libsdp."""
         self.args, self.config = args, config
+        self._score, self.ops = score, ops
         self.device = getattr(config, "device", None) or torch.device("cuda", torch.cuda.current_device())
         sim = getattr(config, "simultaneous", None)
         g = (lambda k, d: getattr(sim, k, d)) if sim is not None else (lambda k, d: d)
@@ -87,6 +115,8 @@ class Runner:
             torch.cuda.synchronize()
 
     def load_score(self):
+        if self._score is not None:
+            return self._score
         c = self.config
         net = ScoreNet(H=c.data.image_size, W=c.data.image_width, ngf=c.model.ngf, channels=c.data.channels,
                        num_classes=c.model.num_classes, precision=getattr(self.args, "precision", "fp32x3"))
@@ -118,8 +148,17 @@ class Runner:
             return tuple(b)
         return fetch
 
+    def _gather(self, t, world):
+        """Rank-ordered concatenation of every rank's [n, ...] CPU tensor (None = no views)."""
+        if world == 1:
+            return t
+        objs = [None] * world
+        torch.distributed.all_gather_object(objs, None if t is None else t.numpy())
+        return torch.from_numpy(np.concatenate([o for o in objs if o is not None]))
+
     def sample(self):
         c = self.config
+        rank, world = _dist()
         B, aB = c.sampling.batch_size, c.sampling.actualBatchSize
         H, W = c.data.image_size, c.data.image_width
         n_mega = B // aB
@@ -137,20 +176,27 @@ class Runner:
         end_point, to_add = aB, 0
         if ds == "KITTI360_im_simultaneous_densification":   # AllForOne:553-558
             end_point, to_add = 2, aB - 2
+        m0, m1 = shard_megabatches(n_mega, rank, world)
+        group = None
+        if world > 1:   # the ranks that hold megabatches share tooHigh (every rank joins new_group)
+            active = [r for r in range(world) if shard_megabatches(n_mega, r, world)[1] > shard_megabatches(n_mega, r, world)[0]]
+            group = torch.distributed.new_group(active)
+        writer = rank == 0
         fetch = self._batch_source(ds, B, aB, H, W)
         for bi in range(n_batches):
             (ref_full, mask_full, sky_full, idx_full, toWorld_full, fromWorld_full, goal, toOG,
              save_arr) = fetch(bi)
             save_num = "".join(str(int(save_arr[m * aB])) + "_" for m in range(n_mega))
             png_id = str(bi) if kitti else save_num      # kitti names the PNGs by batchesToDo (kitti:534,661)
-            np.save(os.path.join(folder, "toWorld_" + save_num), toWorld_full.numpy())
-            np.save(os.path.join(folder, "fromWorld_" + save_num), toOG.numpy())
+            if writer:
+                np.save(os.path.join(folder, "toWorld_" + save_num), toWorld_full.numpy())
+                np.save(os.path.join(folder, "fromWorld_" + save_num), toOG.numpy())
             for do in range(end_point):
-                init = torch.rand(B, c.data.channels, H, W, device=self.device)
+                init = torch.rand(B, c.data.channels, H, W, device=self.device)   # same seed on every rank
                 ref = ref_full.float().to(self.device)
                 mask = mask_full.int().to(self.device)
                 sky, toWorld, fromWorld = sky_full.clone(), toWorld_full.clone(), fromWorld_full.clone()
-                if do == 0:
+                if do == 0 and writer:
                     inp = to_grid_layout(inverse_data_transform(ref_full * mask_full))
                     self._png(inp, f"{do}_{png_id}_Input_image_grid_{ck}.png", int(np.sqrt(B)))
                     np.save(os.path.join(folder, f"{do}_{save_num}_Input_completion_{ck}.pth"), inp.numpy())
@@ -169,27 +215,38 @@ class Runner:
                 if k < aB:
                     init, ref, mask = (_first_views(t, n_mega, aB, k) for t in (init, ref, mask))
                     sky, toWorld, fromWorld = (_first_views(t, n_mega, aB, k) for t in (sky, toWorld, fromWorld))
+                n_views = init.shape[0]
+                v0, v1 = m0 * k, m1 * k                     # this rank's views (whole megabatches)
+                sl = slice(v0, v1)
                 self._sync()
                 t0 = time.time()
-                if baseline:
-                    outs, _ = anneal_Langevin_dynamics_inpainting(init, ref, mask, score, sigmas, c.sampling.n_steps_each,
-                                                                  c.sampling.step_lr, denoise=c.sampling.denoise,
-                                                                  grad_ref=1, sampling_step=4)
-                elif kitti:
-                    outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
-                        init, ref, mask, sky, None, self.start_step, self.setting, self.allowance, score, sigmas,
-                        fromWorld, toWorld, k, c.sampling.n_steps_each, c.sampling.step_lr, existMask=ex,
-                        denoise=c.sampling.denoise, grad_ref=self.grad_ref, correlation_coefficient=self.cc,
-                        sampling_step=4)
-                else:
-                    mods = torch.from_numpy(np.array(c.data.modifications))
-                    outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic(
-                        init, ref, mask, sky, None, self.start_step, self.setting, score, sigmas, mods, k,
-                        c.sampling.n_steps_each, c.sampling.step_lr, existMask=ex, denoise=c.sampling.denoise,
-                        grad_ref=self.grad_ref, correlation_coefficient=self.cc, sampling_step=4)
+                outs = None
+                if v1 > v0:
+                    common = dict(noise_views=(v0, n_views), ops=self.ops)
+                    if baseline:
+                        outs, _ = anneal_Langevin_dynamics_inpainting(
+                            init[sl], ref[sl], mask[sl], score, sigmas, c.sampling.n_steps_each, c.sampling.step_lr,
+                            denoise=c.sampling.denoise, grad_ref=1, sampling_step=4, **common)
+                    elif kitti:
+                        outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
+                            init[sl], ref[sl], mask[sl], sky[sl], None, self.start_step, self.setting, self.allowance,
+                            score, sigmas, fromWorld[sl], toWorld[sl], k, c.sampling.n_steps_each, c.sampling.step_lr,
+                            existMask=ex[sl], denoise=c.sampling.denoise, grad_ref=self.grad_ref,
+                            correlation_coefficient=self.cc, sampling_step=4, dist_group=group, **common)
+                    else:
+                        mods = torch.from_numpy(np.array(c.data.modifications))
+                        outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic(
+                            init[sl], ref[sl], mask[sl], sky[sl], None, self.start_step, self.setting, score, sigmas,
+                            mods, k, c.sampling.n_steps_each, c.sampling.step_lr, existMask=ex[sl],
+                            denoise=c.sampling.denoise, grad_ref=self.grad_ref, correlation_coefficient=self.cc,
+                            sampling_step=4, dist_group=group, **common)
+                final = self._gather(None if outs is None else outs[-1], world)
+                shared = None if kitti else self._gather(None if outs is None else outs[-2], world)
                 self._sync()
                 time_taken[do] += time.time() - t0
-                logging.info("--- %s seconds --- (doThis %d, %d views)", time_taken[do] / (bi + 1), do, init.shape[0])
+                if not writer:
+                    continue
+                logging.info("--- %s seconds --- (doThis %d, %d views)", time_taken[do] / (bi + 1), do, n_views)
                 np.save(os.path.join(folder, f"{do}_{save_num}_TimeTaken.npy"), time_taken[do])
                 # grid width: sqrt of the views sampled (kitti:859-870, AllForOne:946-991)
                 if baseline and not kitti:
@@ -198,12 +255,177 @@ class Runner:
                     nrow = int(np.sqrt((do + 2) * n_mega))
                 else:
                     nrow = int(np.sqrt(B))
-                sample = inverse_data_transform(outs[-1].view(init.shape[0], c.data.channels, H, W))
+                sample = inverse_data_transform(final.view(n_views, c.data.channels, H, W))
                 self._png(to_grid_layout(sample), f"{do}_{png_id}_Masked_image_grid_{ck}.png", nrow)
                 np.save(os.path.join(folder, f"{do}_{save_num}_Masked_completion_{ck}.pth"),
                         to_grid_layout(sample).numpy())
                 if not kitti:   # AllForOne:971-988: all_outputs[-2] (last merge image / denoised)
-                    shared = inverse_data_transform(outs[-2].view(init.shape[0], c.data.channels, H, W))
+                    shared = inverse_data_transform(shared.view(n_views, c.data.channels, H, W))
                     self._png(to_grid_layout(shared), f"{do}_{png_id}_Shared_image_grid_initial{ck}.png", nrow)
                     np.save(os.path.join(folder, f"{do}_{save_num}_Shared_completion_initial{ck}.pth"),
                             to_grid_layout(shared).numpy())
+
+    # ------------------------------------------------------------------------------ training
+    def _train_source(self, Bt, rank, world):
+        """Training batches of the (X, mask, sky) triple the loop unpacks (kitti:179).  The
+        datasets now return the 9-tuple of kitti360_im_8Batch.py:304 (the reference's 3-tuple
+        return is commented out, kitti360_im_simultenous_densification.py:338-339), so its first
+        three items are taken -- the reference's loop would fail to unpack it.  Ranks draw
+        disjoint batches (rank r takes batches r, r + world, ...)."""
+        c = self.config
+        H, W = c.data.image_size, c.data.image_width
+        root = getattr(self.args, "kitti_root", None)
+        if not root:
+            seed = getattr(self.args, "seed", 1234)
+
+            def synth(i):
+                sc = synthetic.scene_views(Bt, H, W, seed=seed + 104729 * (i * world + rank))
+                ref, mask = torch.from_numpy(sc["ref"]), torch.from_numpy(sc["mask"])
+                return ref * mask, mask, torch.from_numpy(sc["sky"])
+            return synth
+        dset = kitti360.get_dataset(c.data.dataset, None, c, split="train", root=root, device=self.device)
+        n_batches = len(dset) // Bt
+        state = {"it": None}
+
+        def fetch(i):
+            if state["it"] is None:
+                state["it"] = iter(kitti360.MySampler(n_batches, Bt, random=True))
+            items = []
+            for _ in range(Bt * world):           # one global batch; this rank keeps its slice
+                try:
+                    items.append(next(state["it"]))
+                except StopIteration:
+                    state["it"] = iter(kitti360.MySampler(n_batches, Bt, random=True))
+                    items.append(next(state["it"]))
+            b = kitti360.collate([dset[j] for j in items[rank * Bt:(rank + 1) * Bt]])
+            return b[0], b[1], b[2]
+        return fetch
+
+    def _initial_state_dict(self):
+        """Random-init weights; with --resume_training the reference's shape-filtered partial
+        load of a list-format checkpoint (kitti:115-128: keys whose shape matches replace the
+        fresh weights, the rest stay random)."""
+        c = self.config
+        sd = synthetic_state_dict(c.model.ngf, c.data.channels, c.model.num_classes)
+        if getattr(self.args, "resume_training", False):
+            path = getattr(self.args, "ckpt", None) or "diffusionNet/checkpoint_148.pth"
+            states = torch.load(path, map_location="cpu", weights_only=True)
+            loaded = 0
+            for key, v in states[0].items():
+                k = key[7:] if key.startswith("module.") else key
+                if k in sd and tuple(v.shape) == tuple(np.shape(sd[k])):
+                    sd[k] = v.detach().cpu().numpy() if torch.is_tensor(v) else v
+                    loaded += 1
+            logging.info("resume: %d of %d tensors loaded from %s (shape-filtered, strict=False)", loaded,
+                         len(states[0]), path)
+        return sd
+
+    def _save_checkpoint(self, trainer, epoch, step):
+        """torch.save([score.state_dict() ('module.'-prefixed, DataParallel), optimizer.state_dict(),
+        epoch, step, ema_helper.state_dict()]) -- kitti:295-306, the list format of ncsn_runner.py:169-179
+        that ``ScoreNet.load_checkpoint`` / the sampler's loader read back."""
+        sd = {"module." + k: v.cpu() for k, v in trainer.state_dict().items()}
+        sd["module.sigmas"] = trainer.net.sigmas.clone()
+        ids = {k: i for i, (k, _, _) in enumerate(trainer.layout)}
+        state = {ids[k]: {"step": torch.tensor(float(trainer.steps)), "exp_avg": a.cpu(), "exp_avg_sq": q.cpu()}
+                 for (k, a), (_, q) in zip(trainer.named_parameters(trainer.exp_avg),
+                                           trainer.named_parameters(trainer.exp_avg_sq))}
+        optim = {"state": state, "param_groups": [{"lr": trainer.lr, "betas": (trainer.beta1, trainer.beta2),
+                                                   "eps": trainer.eps, "weight_decay": 0.0, "amsgrad": False,
+                                                   "params": list(range(len(trainer.layout)))}]}
+        states = [sd, optim, epoch, step]
+        if trainer.shadow is not None:
+            states.append({k: v.cpu() for k, v in trainer.ema_state_dict().items()})
+        os.makedirs(self.args.log_path, exist_ok=True)
+        torch.save(states, os.path.join(self.args.log_path, "checkpoint_{}.pth".format(step)))
+        torch.save(states, os.path.join(self.args.log_path, "checkpoint.pth"))
+
+    def _test_loss(self, trainer, test_batch, sigmas, max_t, gen):
+        """The every-100-steps EMA evaluation (kitti:240-290): the curriculum's timesteps on a
+        test batch with the EMA weights, mean DSM loss (no gradient)."""
+        from .training import dsm_loss_value
+        c = self.config
+        ema_net = ScoreNet(H=c.data.image_size, W=c.data.image_width, ngf=c.model.ngf, channels=c.data.channels,
+                           num_classes=c.model.num_classes, precision=trainer.net.precision)
+        sd = trainer.ema_state_dict() if trainer.shadow is not None else trainer.state_dict()
+        sd["sigmas"] = trainer.net.sigmas
+        ema_net.load_state_dict(sd)
+        X, y, _ = (t.to(self.device) for t in test_batch)
+        X, y = X.float(), y.float()
+        sig = torch.as_tensor(sigmas, dtype=torch.float32, device=self.device)
+        orig = X.clone()
+        B = X.shape[0]
+        X = X + torch.randn(X.shape, device=X.device, generator=gen) * sig[0] * torch.logical_not(y).int()
+        total = 0.0
+        for t in range(max_t):
+            used = sig[t].view(1, 1, 1, 1).expand(B, 1, 1, 1)
+            noise = torch.randn(X.shape, device=X.device, generator=gen) * used
+            X = X + noise * y
+            labels = torch.full((B,), t, device=X.device, dtype=torch.int64)
+            grad = ema_net(X.contiguous(), labels)
+            total += float(dsm_loss_value(grad, used, noise, y))
+            step_size = float(c.sampling.step_lr * (float(sig[t]) / float(sig[-1])) ** 2)
+            for _ in range(c.sampling.n_steps_each):
+                pred = X + step_size * grad + torch.randn(X.shape, device=X.device, generator=gen) * np.sqrt(step_size * 2)
+                X = orig * y + pred * torch.logical_not(y).int()
+        return total / max_t
+
+    def train(self):
+        """kitti:83-348 on libsdp: per batch, the curriculum over maxTimeStepReachable (one more
+        timestep every 20 true steps, kitti:292-294), each timestep = noise the known pixels at
+        sigma[t], masked DSM loss, 5 Langevin predictions of the unknown pixels, backward, Adam,
+        EMA; the EMA test loss every 100 steps; list-format checkpoints every snapshot_freq true
+        steps (kitti:295-306); stops at n_iters.  Data parallel: one process per GPU, each rank its
+        own batch of training.batch_size images, gradients averaged over ranks by one RCCL
+        all-reduce (the reference's DataParallel splits one batch instead -- DESIGN §6)."""
+        from .training import get_optimizer, train_step
+        c = self.config
+        rank, world = _dist()
+        group = torch.distributed.group.WORLD if world > 1 else None
+        if getattr(c.training, "snapshot_sampling", False):
+            raise NotImplementedError("training.snapshot_sampling runs the unconditional anneal_Langevin_dynamics "
+                                      "(models/__init__.py:20-57), which is outside this path")
+        precision = getattr(self.args, "precision", "fp32x3")
+        if precision == "fp32":
+            raise ValueError("training runs in --precision fp32x3 or bf16")
+        net = ScoreNet(H=c.data.image_size, W=c.data.image_width, ngf=c.model.ngf, channels=c.data.channels,
+                       num_classes=c.model.num_classes, precision=precision)
+        net.load_state_dict(self._initial_state_dict())
+        trainer = get_optimizer(c, net, dist_group=group)
+        sigmas = get_sigmas_np(c.model.sigma_begin, c.model.sigma_end, c.model.num_classes, c.model.sigma_dist)
+        sig = torch.as_tensor(sigmas, dtype=torch.float32, device=self.device)
+        Bt = c.training.batch_size
+        source = self._train_source(Bt, rank, world)
+        gen = torch.Generator(device=self.device).manual_seed(getattr(self.args, "seed", 1234) + rank)
+        max_epochs = getattr(self.args, "max_epochs", None) or c.training.n_epochs
+        batches_per_epoch = getattr(self.args, "num_batches", None) or 1
+        step = true_step = 0
+        max_t = 1
+        self.losses = []
+        for epoch in range(max_epochs):
+            for i in range(batches_per_epoch):
+                step += 1
+                X, mask, sky = source(epoch * batches_per_epoch + i)
+                X = X.float().to(self.device)
+                mask = mask.float().to(self.device)
+                original = X.clone()
+                # max noise into the untrusted pixels (kitti:183-186)
+                X = X + torch.randn(X.shape, device=X.device, generator=gen) * sig[0] * torch.logical_not(mask).int()
+                for t in range(max_t):
+                    true_step += 1
+                    loss, X = train_step(trainer, X, original, mask, sigmas, t, c.sampling.step_lr,
+                                         c.sampling.n_steps_each, c.training.anneal_power, generator=gen)
+                    lv = float(loss)
+                    self.losses.append(lv)
+                    if rank == 0:
+                        logging.info("step: {}, timestep: {}, loss: {}".format(step, t, lv))
+                    if step >= c.training.n_iters:
+                        return 0
+                    if step % 100 == 0 and t == 0 and rank == 0:
+                        tl = self._test_loss(trainer, source(10 ** 6 + step), sigmas, max_t, gen)
+                        logging.info("step: {}, test_loss: {}".format(step, tl))
+                    if true_step % 20 == 0 and max_t < len(sigmas):
+                        max_t += 1
+                    if true_step % c.training.snapshot_freq == 0 and rank == 0:
+                        self._save_checkpoint(trainer, epoch, step)
+        return 0

@@ -10,7 +10,9 @@ tensor), the fused Langevin kernel (update + max|x[:,0]| for tooHigh), and -- fr
 scale, correlation ramps) are computed with the reference's numpy float32 arithmetic.
 
 Keyword-only extras (not in the reference): ``noise_fn(shape) -> tensor`` injects the
-noise (parity tests); otherwise noise is Philox N(0,1) from ``seed``.  ``dist_group`` makes
+noise (parity tests); otherwise noise is Philox N(0,1) from ``seed``, one counter per 4
+elements of the whole job, so ``noise_views=(first_view, total_views)`` lets a call that
+holds a contiguous slice of a larger job (megabatch sharding) draw that slice's noise.  ``dist_group`` makes
 tooHigh global across ranks (one 4-byte all_reduce(MAX) per merged step); with
 ``view_shard=(rank, world)`` the call's views are one megabatch split across ranks: each
 rank passes only its own views, the megabatch images are all-gathered every merged step
@@ -53,7 +55,7 @@ class _Stepper:
     """Per-call state shared by the samplers.  ``x`` is this rank's views; with a view shard
     it is a contiguous slice of ``x_all`` (the whole megabatch)."""
 
-    def __init__(self, x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all=None, own0=0):
+    def __init__(self, x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all=None, own0=0, noise_views=None):
         self.ops = ops
         x = x_mod.detach().to(torch.float32).contiguous()
         self.B, self.C, self.H, self.W = x.shape
@@ -72,9 +74,11 @@ class _Stepper:
         self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
         # Philox counters are per 4 elements of the WHOLE megabatch: a rank holding views
         # [own0, own0+B) draws exactly the noise the single-process run draws for those views
+        # (noise_views = (first view, views of the whole job) when the job is split by megabatch)
+        nv0, nv_all = noise_views if noise_views is not None else (own0, n_all)
         self.per_view4 = self.C * self.H * self.W // 4
-        self.offset = own0 * self.per_view4
-        self.offset_stride = n_all * self.per_view4
+        self.offset = nv0 * self.per_view4
+        self.offset_stride = nv_all * self.per_view4
         self._labels = {}
 
     def labels(self, c):
@@ -120,9 +124,9 @@ def _step_size(step_lr, sigma, sigma_last):
 @torch.no_grad()
 def anneal_Langevin_dynamics_inpainting(x_mod, refer_image, refer_mask, scorenet, sigmas, n_steps_each=100,
                                         step_lr=0.000008, denoise=True, verbose=True, grad_ref=0.1, sampling_step=16,
-                                        *, noise_fn=None, seed=1234, keep_all=False, ops=None):
+                                        *, noise_fn=None, seed=1234, keep_all=False, ops=None, noise_views=None):
     """Single-view baseline (models/__init__.py:1385-1442). No nan_to_num, as in the reference."""
-    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops or DeviceOps())
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops or DeviceOps(), noise_views=noise_views)
     sigmas = np.asarray(sigmas, dtype=np.float32)
     images, targets = [], []
     last = None
@@ -209,7 +213,7 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
         x_mod, refer_image, refer_mask, sky, x_indices, minStepToShare, setting, allowance, scorenet, sigmas, fromWorld,
         toWorld, actualBatchSize, n_steps_each=100, step_lr=0.000008, existMask=None, denoise=True, verbose=True,
         grad_ref=0.1, correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None,
-        view_shard=None, all_refer_mask=None, all_sky=None, ops=None):
+        view_shard=None, all_refer_mask=None, all_sky=None, ops=None, noise_views=None):
     """Pose-matrix simultaneous sampler (KITTISampling.py:6-513); x_indices/sampling_step unused as there.
 
     With ``view_shard=(rank, world)``: x_mod/refer_* hold this rank's views, while fromWorld,
@@ -217,7 +221,7 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
     """
     ops = ops or DeviceOps()
     n_all, own0 = _shard_setup(x_mod, actualBatchSize, view_shard)
-    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0)
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0, noise_views)
     sky_all = sky if view_shard is None else all_sky
     mask_all = S.mask if view_shard is None else all_refer_mask
     merger = ops.make_merger(n_all, actualBatchSize, S.H, S.W, S.dev, existMask, sky_all, mask_all, toWorld=toWorld,
@@ -240,11 +244,11 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic(
         x_mod, refer_image, refer_mask, sky, x_indices, minStepToShare, setting, scorenet, sigmas, modificationList,
         actualBatchSize, n_steps_each=100, step_lr=0.000008, existMask=None, denoise=True, verbose=True, grad_ref=0.1,
         correlation_coefficient=0.1, sampling_step=16, *, noise_fn=None, seed=1234, dist_group=None, view_shard=None,
-        all_refer_mask=None, all_sky=None, ops=None):
+        all_refer_mask=None, all_sky=None, ops=None, noise_views=None):
     """Origin-offset (AllForOne) simultaneous sampler (models/__init__.py:112-602)."""
     ops = ops or DeviceOps()
     n_all, own0 = _shard_setup(x_mod, actualBatchSize, view_shard)
-    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0)
+    S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0, noise_views)
     sky_all = sky if view_shard is None else all_sky
     mask_all = S.mask if view_shard is None else all_refer_mask
     origins = allforone_origins(modificationList)

@@ -164,6 +164,16 @@ def anneal_dsm_score_estimation_with_mask(scorenet: Trainer, perturbed_samples, 
     return loss, scores
 
 
+def dsm_loss_value(scores, used_sigmas, noise, masks, anneal_power=2.0):
+    """losses/dsm.py:80-93 as device torch ops, for evaluation (no gradient): the runner's test loss."""
+    B = scores.shape[0]
+    target = -1 / (used_sigmas ** 2) * noise
+    m = masks.reshape(B, -1).float()
+    diff = m * (scores.reshape(B, -1) - target.reshape(B, -1))
+    loss = 0.5 * (diff ** 2).sum(dim=-1) * (scores[0].numel() / m.sum()) * used_sigmas.reshape(B) ** anneal_power
+    return loss.mean()
+
+
 def get_optimizer(config, net: ScoreNet, **kw) -> Trainer:
     """losses/__init__.py:10-20 (Adam only: the shipped configs' optimizer)."""
     o = config.optim

@@ -29,13 +29,20 @@ class OracleMerger:
         self.exist = np.asarray(exist)
         self.sky = np.asarray(sky).reshape(n_all, 1, H, W)
         self.refmask = np.asarray(refmask)
-        self.toWorld = np.asarray(toWorld).reshape(n_all, 4, 4)
-        self.fromWorld = np.asarray(fromWorld).reshape(n_all, 4, 4)
+        # origin-offset variant: the origins are already 10*sign(m), which the oracle maps to themselves
+        self.mods = None if origins is None else np.asarray(origins)
+        if origins is None:
+            self.toWorld = np.asarray(toWorld).reshape(n_all, 4, 4)
+            self.fromWorld = np.asarray(fromWorld).reshape(n_all, 4, 4)
 
     def __call__(self, x_all, sigma, setting, allowance, cc, absmax, new):
         amax = absmax.view(torch.float32).item()
-        n, xc = S.kitti_merge(x_all.numpy(), self.refmask, self.sky, self.exist, self.toWorld, self.fromWorld,
-                              self.aB, sigma, setting, allowance, cc, absmax=amax)
+        if self.mods is not None:
+            n, xc = S.allforone_merge(x_all.numpy(), self.refmask, self.sky, self.exist, self.mods, self.aB, sigma,
+                                      setting, cc, absmax=amax)
+        else:
+            n, xc = S.kitti_merge(x_all.numpy(), self.refmask, self.sky, self.exist, self.toWorld, self.fromWorld,
+                                  self.aB, sigma, setting, allowance, cc, absmax=amax)
         sl = slice(self.o_begin, self.o_begin + self.n_out)
         x_all[sl] = torch.from_numpy(xc[sl])
         if new is not None:

@@ -41,7 +41,7 @@ def _args(folder):
 def calls(monkeypatch):
     log = []
 
-    def base(init, ref, mask, score, sigmas, n, lr, denoise=True, grad_ref=1, sampling_step=4):
+    def base(init, ref, mask, score, sigmas, n, lr, denoise=True, grad_ref=1, sampling_step=4, **kw):
         log.append(("baseline", init.shape[0], None))
         return [init + 0.25, init + 0.5, init * 2], []
 
