@@ -397,7 +397,7 @@ class Runner:
         Bt = c.training.batch_size
         source = self._train_source(Bt, rank, world)
         gen = torch.Generator(device=self.device).manual_seed(getattr(self.args, "seed", 1234) + rank)
-        max_epochs = getattr(self.args, "max_epochs", None) or c.training.n_epochs
+        max_epochs = getattr(self.args, "max_epochs", None) or getattr(c.training, "n_epochs", 500000)
         batches_per_epoch = getattr(self.args, "num_batches", None) or 1
         step = true_step = 0
         max_t = 1
