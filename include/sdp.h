@@ -23,6 +23,8 @@
  *   sdp_view_transform     pose chain fromWorld @ (toWorld @ p)             datasets/kitti360_im_8Batch.py:146-190
  *   sdp_view_gather        scanPoints[index[index >= 0]]                    datasets/kitti360_im_simultenous_densification.py:186-203
  *   sdp_view_finalize      __getitem__ post-processing of the range images  datasets/kitti360_im_8Batch.py:221-304
+ *   sdp_grid_subsample     voxel-grid subsampling (HOST)                    datasets/cpp_wrappers/cpp_subsampling/
+ *                                                                             grid_subsampling{,_lidar}.cpp, wrapper.cpp:58-285
  */
 #ifndef SDP_H
 #define SDP_H
@@ -180,8 +182,11 @@ int sdp_range_project(const double* points, int N, int stride, int has_intensity
  *   Inputs are sdp_range_project outputs of the view and of the goal scan ([H][W], DEVICE;
  *   intensity / goal_intensity only with channels == 2); roll = the random_roll column shift
  *   or -1.  Outputs DEVICE: real, goal float64 [channels][H][W], notmask u8 [channels][H][W]
- *   (np.logical_not(mask)), notsky u8 [H][W] (np.logical_not(sky) after the 3-row shift).   */
-enum sdp_view_variant { SDP_VIEW_8BATCH = 0, SDP_VIEW_ALLFORONE = 1, SDP_VIEW_DENSIFICATION = 2 };
+ *   (np.logical_not(mask)), notsky u8 [H][W] (np.logical_not(sky) after the 3-row shift).
+ *   SDP_VIEW_COMPLETION: kitti360_im_SceneCompletion.py:388-513 -- channel 2 of real is the
+ *   depth code again and its mask is all ones (the reference concatenates (real, real) and
+ *   (mask, ones)); goal_depth / goal_intensity / goal may be NULL (no goal scan).            */
+enum sdp_view_variant { SDP_VIEW_8BATCH = 0, SDP_VIEW_ALLFORONE = 1, SDP_VIEW_DENSIFICATION = 2, SDP_VIEW_COMPLETION = 3 };
 int sdp_view_transform(const float* points, int64_t n, const double* m1, const double* m2, double* out, void* stream);
 int sdp_view_gather(const int64_t* index, int H, int W, int blank_cols, const float* points, double* out, int* count,
                     void* stream);
@@ -189,6 +194,17 @@ int sdp_view_finalize(const double* depth, const double* intensity, const uint8_
                       const double* goal_depth, const double* goal_intensity, int H, int W, int channels, int roll,
                       int variant, int first_view, double* real, uint8_t* notmask, uint8_t* notsky, double* goal,
                       void* stream);
+
+/* ---- §8(f)-3: voxel-grid subsampling, HOST memory (no stream) ------------------------------
+ * sdp_grid_subsample replaces the CPython modules grid_subsampling.compute (method 0,
+ *   "barycenters": grid_subsampling.cpp:46-102) and grid_subsampling_lidar.compute (method 1:
+ *   grid_subsampling_lidar.cpp:46-120), wrapper.cpp:58-285.  points float32 [n][3], features
+ *   float32 [n][fdim] or NULL, classes int32 [n][ldim] or NULL, voxel size sample_dl.  Outputs
+ *   (capacity n rows each): out_points [m][3], out_features [m][fdim], out_classes [m][ldim];
+ *   *out_n = m, in the reference's voxel order (see csrc/grid_subsampling.cpp).             */
+int sdp_grid_subsample(const float* points, int64_t n, const float* features, int fdim, const int32_t* classes,
+                       int ldim, float sample_dl, int method, float* out_points, float* out_features,
+                       int32_t* out_classes, int64_t* out_n);
 
 #ifdef __cplusplus
 }

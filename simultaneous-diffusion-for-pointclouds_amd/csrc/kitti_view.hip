@@ -123,12 +123,17 @@ __global__ __launch_bounds__(256) void view_finalize_kernel(FinalizeArgs a) {
   const int sr = r >= 3 ? r - 3 : 0;
   a.notsky[i] = a.sky[sr * a.W + sc] ? 0 : 1;
   a.real[i] = depth_code(d);
-  a.goal[i] = depth_code(a.goal_depth[i]);
+  if (a.goal) a.goal[i] = depth_code(a.goal_depth[i]);
   a.notmask[i] = m ? 0 : 1;
   if (a.C == 2) {
-    a.real[HW + i] = inten_code(a.inten[s]);
-    a.goal[HW + i] = inten_code(a.goal_inten[i]);
-    a.notmask[HW + i] = m ? 0 : 1;
+    if (a.variant == SDP_VIEW_COMPLETION) {   // SceneCompletion: (real, real) and (mask, ones)
+      a.real[HW + i] = a.real[i];
+      a.notmask[HW + i] = 0;
+    } else {
+      a.real[HW + i] = inten_code(a.inten[s]);
+      a.notmask[HW + i] = m ? 0 : 1;
+    }
+    if (a.goal) a.goal[HW + i] = inten_code(a.goal_inten[i]);
   }
 }
 
@@ -167,9 +172,11 @@ int sdp_view_finalize(const double* depth, const double* intensity, const uint8_
                       const double* goal_depth, const double* goal_intensity, int H, int W, int channels, int roll,
                       int variant, int first_view, double* real, uint8_t* notmask, uint8_t* notsky, double* goal,
                       void* stream) {
-  if (!depth || !obfuscation || !sky || !goal_depth || !real || !notmask || !notsky || !goal || H < 1 || W < 1 ||
-      (channels != 1 && channels != 2) || (channels == 2 && (!intensity || !goal_intensity)) || roll >= W ||
-      variant < SDP_VIEW_8BATCH || variant > SDP_VIEW_DENSIFICATION)
+  const bool has_goal = goal != nullptr;
+  if (!depth || !obfuscation || !sky || !real || !notmask || !notsky || H < 1 || W < 1 ||
+      (has_goal && !goal_depth) || (variant != SDP_VIEW_COMPLETION && !has_goal) ||
+      (channels != 1 && channels != 2) || (channels == 2 && (!intensity || (has_goal && !goal_intensity))) ||
+      roll >= W || variant < SDP_VIEW_8BATCH || variant > SDP_VIEW_COMPLETION)
     return sdp_fail("sdp_view_finalize: bad argument");
   sdp::FinalizeArgs a{depth, intensity, goal_depth, goal_intensity, obfuscation, sky, real, goal, notmask, notsky,
                       H, W, channels, roll, variant, first_view};

@@ -59,6 +59,7 @@ _SIGS = {
     "sdp_view_transform": (I, [P, C.c_int64, P, P, P, P]),
     "sdp_view_gather": (I, [P, I, I, I, P, P, P, P]),
     "sdp_view_finalize": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P, P]),
+    "sdp_grid_subsample": (I, [P, C.c_int64, P, I, P, I, F, I, P, P, P, C.POINTER(C.c_int64)]),
     "sdp_langevin_step": (I, [P, P, P, P, P, U64, U64, F, F, F, I, I, I, I, P, P, P]),
     "sdp_axpy_step": (I, [P, P, F, P, P, P, F, I, P]),
     "sdp_merge_workspace_size": (I, [I, I, I, I, C.POINTER(SZ)]),

@@ -157,6 +157,8 @@ class Runner:
         return torch.from_numpy(np.concatenate([o for o in objs if o is not None]))
 
     def sample(self):
+        if self.config.data.dataset == "kitti360_im_SceneCompletion":
+            return self.sample_completion()
         c = self.config
         rank, world = _dist()
         B, aB = c.sampling.batch_size, c.sampling.actualBatchSize
@@ -264,6 +266,98 @@ class Runner:
                     self._png(to_grid_layout(shared), f"{do}_{png_id}_Shared_image_grid_initial{ck}.png", nrow)
                     np.save(os.path.join(folder, f"{do}_{save_num}_Shared_completion_initial{ck}.pth"),
                             to_grid_layout(shared).numpy())
+
+    # ------------------------------------------------------------------------------ scene completion
+    def _completion_source(self, B, aB, H, W):
+        """bi -> the DataLoader's 6-tuple (real, notmask, notsky, index, names, origins) for batch
+        bi: the SSC dataset of sdp.completion with --kitti_root (MySampler(valSize, actualBatchSize,
+        random=False), Completion:500-504), else procedural views (origins = the view positions)."""
+        from . import completion
+        root = getattr(self.args, "kitti_root", None)
+        if not root:
+            seed = getattr(self.args, "seed", 1234)
+
+            def synth(bi):
+                sc = synthetic.scene_views(B, H, W, seed=seed + 7919 * bi)
+                ref, mask = torch.from_numpy(sc["ref"]), torch.from_numpy(sc["mask"])
+                origins = torch.from_numpy(sc["toWorld"][:, :3, 3]).unsqueeze(1)
+                idx = torch.zeros(B, 1, H, W, dtype=torch.float64)
+                # (the dataset's masks come back logical_not-ed: True = known pixel / not sky)
+                return ref.double(), mask.bool(), torch.from_numpy(sc["sky"]), idx, [f"{bi:06d}"] * B, origins
+            return synth, 1
+        dset = completion.kitti360_im_SceneCompletion(None, self.config, split="test", root=root, device=self.device)
+        n_val = completion.val_size(root)
+        order = iter(kitti360.MySampler(n_val, aB, random=False))
+
+        def fetch(bi):
+            return completion.collate([dset[next(order)] for _ in range(B)])
+        return fetch, n_val
+
+    def sample_completion(self):
+        """runners/ncsn_runner_Completion.py:468-940 (inpainting, final_only): per batch of
+        sampling.batch_size views, doThis 0 saves the inputs (Input grid/npy, SKY, ORIGINS) and
+        samples nothing; doThis 1 runs the origin-offset simultaneous sampler with the dataset's
+        per-view origins (startStep 2, setting 7, correlation 0.01, grad_ref 1, Completion:548-566)
+        and saves TimeTaken, the Masked and the Shared (last merge) images.  Quirks kept: the
+        dataset's mask (True = known after logical_not) multiplies the input as in the reference,
+        TimeTaken starts at 999999 (L512), the Shared files are named by the batch counter."""
+        c = self.config
+        rank, world = _dist()
+        B, aB = c.sampling.batch_size, c.sampling.actualBatchSize
+        H, W = c.data.image_size, c.data.image_width
+        score = self.load_score()
+        sigmas = get_sigmas_np(c.model.sigma_begin, c.model.sigma_end, c.model.num_classes, c.model.sigma_dist)
+        ex = torch.from_numpy(np.broadcast_to(synthetic.exist_mask(H, W), (B, H, W)).copy())
+        folder = self.args.image_folder
+        ck = c.sampling.ckpt_id
+        fetch, n_val = self._completion_source(B, aB, H, W)
+        n_batches = min(getattr(self.args, "num_batches", 1) or n_val, n_val)
+        time_taken = np.zeros(max(n_val, 2)) + 999999
+        writer = rank == 0
+        group = torch.distributed.group.WORLD if world > 1 else None
+        n_mega = B // aB
+        m0, m1 = shard_megabatches(n_mega, rank, world)
+        if world > 1 and not all(shard_megabatches(n_mega, r, world)[1] > shard_megabatches(n_mega, r, world)[0]
+                                 for r in range(world)):
+            raise ValueError(f"scene completion: {n_mega} megabatches cannot feed {world} ranks")
+        for bi in range(n_batches):
+            ref_full, mask_full, sky_full, idx_full, names, origins = fetch(bi)
+            save_num = names[0]
+            for do in range(2):
+                init = torch.rand(B, c.data.channels, H, W, device=self.device)
+                ref = ref_full.float().to(self.device)
+                mask = mask_full.int().to(self.device)
+                refer = to_grid_layout(inverse_data_transform(ref_full * mask_full))
+                if do == 0:
+                    if writer:
+                        self._png(refer, f"{do}_{save_num}_Input_image_grid_{ck}.png", int(np.sqrt(B)))
+                        np.save(os.path.join(folder, f"{do}_{save_num}_Input_completion_{ck}.pth"), refer.numpy())
+                        np.save(os.path.join(folder, f"{do}_{save_num}_SKY_{ck}.pth"), sky_full.numpy())
+                        np.save(os.path.join(folder, f"{do}_{save_num}_ORIGINS_{ck}.pth"), origins.numpy())
+                    continue
+                mods = torch.squeeze(origins).reshape(B, 3)
+                sl = slice(m0 * aB, m1 * aB)
+                self._sync()
+                t0 = time.time()
+                outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic(
+                    init[sl], ref[sl], mask[sl], sky_full[sl], None, 2, 7, score, sigmas, mods, aB,
+                    c.sampling.n_steps_each, c.sampling.step_lr, existMask=ex[sl], denoise=c.sampling.denoise,
+                    grad_ref=1, correlation_coefficient=0.01, sampling_step=4, dist_group=group,
+                    noise_views=(sl.start, B), ops=self.ops)
+                final = self._gather(outs[-1], world)
+                shared = self._gather(outs[-2], world)
+                self._sync()
+                time_taken[do] += time.time() - t0
+                if not writer:
+                    continue
+                np.save(os.path.join(folder, f"{do}_{save_num}_TimeTaken.npy"), time_taken[do])
+                sample = to_grid_layout(inverse_data_transform(final.view(B, c.data.channels, H, W)))
+                initial = to_grid_layout(inverse_data_transform(shared.view(B, c.data.channels, H, W)))
+                nrow = int(np.sqrt(B))
+                self._png(sample, f"{do}_{save_num}_Masked_image_grid_{ck}.png", nrow)
+                np.save(os.path.join(folder, f"{do}_{save_num}_Masked_completion_{ck}.pth"), sample.numpy())
+                self._png(initial, f"{do}_{bi}_Shared_image_grid_initial{ck}.png", nrow)
+                np.save(os.path.join(folder, f"{do}_{bi}_Shared_completion_initial{ck}.pth"), initial.numpy())
 
     # ------------------------------------------------------------------------------ training
     def _train_source(self, Bt, rank, world):
