@@ -66,6 +66,7 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (a.Cin > 1024 && a.ss_bstride == 0) { *why = "conv: identity table holds 1024 channels"; return hipErrorInvalidValue; }
 #ifdef SDP_CONV_BENCH_ONLY
   if (mode == MODE_BF16) return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st);
+  if (mode == MODE_F32) return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
   return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
 #endif
   switch (mode) {

@@ -44,6 +44,14 @@ namespace sdp {
 #define SDP_KO 0
 #endif
 
+// cache-policy bits (aux) of the patch LDS-DMA loads and of the forward epilogue stores
+#ifndef SDP_DMA_AUX
+#define SDP_DMA_AUX 0
+#endif
+#ifndef SDP_STORE_AUX
+#define SDP_STORE_AUX 2   // nt: the output streams to HBM without displacing the L2-resident weights
+#endif                    // (conv_bench 256->256 @32x512: 218 -> 214 us, tools/aux_run.sh)
+
 #ifdef SDP_TIMING   // tools/conv_bench: per-workgroup phase clocks of wave 0 into a.dbg
 #define SDP_T(i) do { if (tid == 0) tclk[i] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
@@ -191,7 +199,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
-        uoff[k], chunk * 128, 0, 0);
+        uoff[k], chunk * 128, 0, SDP_DMA_AUX);
   };
   // transform staging unit k of raw into patch buffer PB
   // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
@@ -694,7 +702,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         }
         if constexpr (!(SDP_KO & 16)) {
   #pragma unroll
-          for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI_OFF(i), 0);
+          for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI_OFF(i), SDP_STORE_AUX);
         }
   #undef SDP_EPI_OFF
         if (a.stats) {

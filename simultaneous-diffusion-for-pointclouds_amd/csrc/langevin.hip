@@ -91,9 +91,17 @@ __global__ __launch_bounds__(256) void langevin_kernel(float* __restrict__ x, co
     }
   }
   if (absmax) {
+    // wave max, then block max in LDS: ONE atomic per block (same-address atomics serialise
+    // at the L2 -- one per wave cost ~10 us of a 16 us launch at 4 views)
+    __shared__ uint32_t wmax[4];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) local_max = max(local_max, (uint32_t)__shfl_xor((int)local_max, off));
-    if ((threadIdx.x & 63) == 0 && local_max) atomicMax(absmax, local_max);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = local_max;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+      if (m) atomicMax(absmax, m);
+    }
   }
 }
 
@@ -118,7 +126,9 @@ hipError_t langevin_step(float* x, const float* g, const float* ref, const int32
                          uint64_t seed, uint64_t offset, float step, float nscale, float gref, int n2n, int B, int C,
                          int HW, float* lik_out, uint32_t* absmax, hipStream_t st) {
   const size_t n4 = (size_t)B * C * HW / 4;
-  hipLaunchKernelGGL(langevin_kernel, dim3(grid_for(n4)), dim3(256), 0, st, x, g, ref, mask, noise, seed, offset, step,
+  // with the absmax reduction: at most 256 blocks (one atomic each), each thread a few float4s
+  const int grid = absmax ? (int)std::min<size_t>((n4 + 255) / 256, 256) : grid_for(n4);
+  hipLaunchKernelGGL(langevin_kernel, dim3(grid), dim3(256), 0, st, x, g, ref, mask, noise, seed, offset, step,
                      nscale, gref, n2n, C, HW, n4, lik_out, absmax);
   return hipGetLastError();
 }
