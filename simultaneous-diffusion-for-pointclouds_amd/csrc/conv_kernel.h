@@ -82,9 +82,17 @@ struct ConvTile {
 
 SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU>
+// SH: MFMA shape of the bf16 modes -- 32 = v_mfma_f32_32x32x16_bf16 (wave tile = 4 x 2 fragments
+// of 32 px x 32 Cout, two 16-deep k steps per 32-channel chunk), 16 = v_mfma_f32_16x16x32_bf16
+// (8 x 4 fragments of 16 px x 16 Cout, one 32-deep k step per chunk).  Same cycles per FLOP; the
+// chip holds a higher clock on the 16x16 shape under this load (MI355X_MICROARCH.md 'DVFS
+// give-back' item 7).  SH = 16 is forward-only (direct epilogue, no dact) and reads the SAME packed
+// weights: a lane fetches the (cout, 8-channel group) its 16x16 fragment needs from the 32x32
+// packing by its own buffer offset.
+template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32>
 __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
+  static_assert(SH == 32 || (SH == 16 && MODE != MODE_F32), "16x16 shape: bf16 modes only");
   using T = ConvTile<WM, TC, KS>;
   constexpr int NT = KS * KS;
   constexpr int NU = T::NU;
@@ -121,12 +129,22 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   const int nbg0 = n0 / 32 + wn * 2;               // global 32-channel block of this wave's nb=0
 
   f32x16 acc[4][2];
-  static_for<0, 4>([&](auto i) {
-    static_for<0, 2>([&](auto j) {
+  f32x4 acc4[8][4];                                // SH == 16: [16-px group][16-Cout group]
+  if constexpr (SH == 32) {
+    static_for<0, 4>([&](auto i) {
+      static_for<0, 2>([&](auto j) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      });
     });
-  });
+  } else {
+    static_for<0, 8>([&](auto i) {
+      static_for<0, 4>([&](auto j) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
+      });
+    });
+  }
 
   // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
   // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
@@ -136,17 +154,39 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   // weight fragment ring: 3 taps deep (prefetch distance 2) when the tap count is a multiple
   // of 3, so the slot of (chunk, tap) is tap % 3 in every chunk; 2 deep for the 1x1 conv
   constexpr int NBUF = (NT % 3 == 0) ? 3 : 2;
-  uint4 bq[NBUF][2][4];
+  uint4 bq[NBUF][2][4];   // SH 32: [slot][nb][(s, hi/lo)]; SH 16: [slot][nj / 2][(nj % 2, hi/lo)]
+  // SH 16: fragment nj (Couts 16 nj .. of the wave's 64) lane l needs Cout 16 nj + l % 16 and
+  // channel group g = l / 16 (channels 8g .. 8g+7 of the chunk); the 32x32 packing stores Cout c,
+  // channels 16 s + 8 h at lane c % 32 + 32 h, slot s -- so the lane reads from there
+  int wq16[4];
+  {
+    const int g = lane >> 4, h = g & 1, sg = g >> 1;
+    static_for<0, 4>([&](auto njc) {
+      constexpr int nj = decltype(njc)::value;
+      const int L = 16 * (nj & 1) + (lane & 15) + 32 * h;
+      wq16[nj] = ((nbg0 + (nj >> 1)) * 64 + L) * 64 + sg * 32;
+    });
+  }
   auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
     constexpr int J = decltype(buf)::value;
     if constexpr (SDP_KO & 4) return;
     const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096);
-    static_for<0, 4>([&](auto q) {
-      const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
-      const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
-      bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
-      bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
-    });
+    if constexpr (SH == 32) {
+      static_for<0, 4>([&](auto q) {
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
+        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
+        bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+        bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+      });
+    } else {
+      static_for<0, 4>([&](auto njc) {
+        constexpr int nj = decltype(njc)::value;
+        const u32x4 vh = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj], so, 0);
+        const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj] + 16, so, 0);
+        bq[J][nj >> 1][2 * (nj & 1)] = make_uint4(vh.x, vh.y, vh.z, vh.w);
+        bq[J][nj >> 1][2 * (nj & 1) + 1] = make_uint4(vl.x, vl.y, vl.z, vl.w);
+      });
+    }
   };
 
   const float* inb = a.in + (size_t)b * a.H * a.W * Cin;
@@ -285,16 +325,27 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   __syncthreads();
   SDP_T(2);
 
-  // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel
+  // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel.
+  // SH 32: s = the 16-deep k step, fragments mb 0..3 (32 px each); SH 16: s = which half of the 8
+  // 16-px fragments (mb 4s .. 4s+3), lane l = pixel l % 16, channels 8 (l / 16) ..
+  const int a_lane_off16 = (lane & 15) * PSTRIDE + (lane >> 4) * 16;
   auto read_a = [&](const char* pat, auto tap_c, auto s_c, bf16x8* hi, bf16x8* lo) __attribute__((always_inline)) {
     constexpr int tap = decltype(tap_c)::value, s = decltype(s_c)::value;
     constexpr int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
     static_for<0, 4>([&](auto mbc) {
-      constexpr int mb = decltype(mbc)::value;
-      constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
-      const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off + s * 32;
-      hi[mb] = *reinterpret_cast<const bf16x8*>(src);
-      if constexpr (MODE == MODE_F32X3) lo[mb] = *reinterpret_cast<const bf16x8*>(src + 64);
+      if constexpr (SH == 32) {
+        constexpr int mb = decltype(mbc)::value;
+        constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
+        const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off + s * 32;
+        hi[mb] = *reinterpret_cast<const bf16x8*>(src);
+        if constexpr (MODE == MODE_F32X3) lo[mb] = *reinterpret_cast<const bf16x8*>(src + 64);
+      } else {
+        constexpr int i = decltype(mbc)::value, mb = 4 * s + i;
+        constexpr int mr = mb / (TC / 16), mc = (mb % (TC / 16)) * 16;
+        const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off16;
+        hi[i] = *reinterpret_cast<const bf16x8*>(src);
+        if constexpr (MODE == MODE_F32X3) lo[i] = *reinterpret_cast<const bf16x8*>(src + 64);
+      }
     });
   };
 
@@ -383,19 +434,35 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         if constexpr (tap + 1 < NT)
           read_a(pat, std::integral_constant<int, tap + 1>{}, std::integral_constant<int, 0>{}, pre_hi, pre_lo);
         if constexpr (NT > 1) dmas();   // 1x1: after the blocks, behind this tap's raw reads
-        static_for<0, 16>([&](auto blk_c) {
+        constexpr int NBLK = SH == 32 ? 16 : 32;
+        static_for<0, NBLK>([&](auto blk_c) {
           constexpr int blk = decltype(blk_c)::value;
-          constexpr int s = blk >> 3, nb = (blk >> 2) & 1, mb = blk & 3;
-          const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
-          const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
-          const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
-          const bf16x8 ahi = s == 0 ? c0_hi[mb] : c1_hi[mb];
-          if constexpr (MODE == MODE_F32X3) {
-            const bf16x8 alo = s == 0 ? c0_lo[mb] : c1_lo[mb];
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[mb][nb], 0, 0, 0);
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[mb][nb], 0, 0, 0);
+          if constexpr (SH == 32) {
+            constexpr int s = blk >> 3, nb = (blk >> 2) & 1, mb = blk & 3;
+            const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
+            const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
+            const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
+            const bf16x8 ahi = s == 0 ? c0_hi[mb] : c1_hi[mb];
+            if constexpr (MODE == MODE_F32X3) {
+              const bf16x8 alo = s == 0 ? c0_lo[mb] : c1_lo[mb];
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[mb][nb], 0, 0, 0);
+              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[mb][nb], 0, 0, 0);
+            }
+            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[mb][nb], 0, 0, 0);
+          } else {
+            // block = (half s of the px groups, Cout group nj, px group i of the half)
+            constexpr int s = blk >> 4, nj = (blk >> 2) & 3, i = blk & 3, mb = 4 * s + i;
+            const uint4 h4 = bq[CUR][nj >> 1][2 * (nj & 1)], l4 = bq[CUR][nj >> 1][2 * (nj & 1) + 1];
+            const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
+            const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
+            const bf16x8 ahi = s == 0 ? c0_hi[i] : c1_hi[i];
+            if constexpr (MODE == MODE_F32X3) {
+              const bf16x8 alo = s == 0 ? c0_lo[i] : c1_lo[i];
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc4[mb][nj], 0, 0, 0);
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc4[mb][nj], 0, 0, 0);
+            }
+            acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc4[mb][nj], 0, 0, 0);
           }
-          acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[mb][nb], 0, 0, 0);
           if constexpr (blk < 2 * NX) xform_piece(std::integral_constant<int, tap + XT * (blk >> 1)>{},
                                                   std::integral_constant<int, blk & 1>{},
                                                   std::integral_constant<int, 1 - P>{}, xv[blk >> 1]);
