@@ -6,12 +6,27 @@
 namespace sdp {
 
 // ----------------------------------------------------------------------------- launch
+// MFMA shape of the forward bf16-mode launches (conv_kernel.h SH): 16 unless SDP_MFMA_SHAPE=32
+static int mfma_shape() {
+  static const int sh = [] {
+    const char* e = getenv("SDP_MFMA_SHAPE");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return sh;
+}
+
 template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
 static hipError_t launch_t(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS>;
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  if constexpr (MODE != MODE_F32) {
+    if (!a.dact && mfma_shape() == 16) {
+      hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16>), grid, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }

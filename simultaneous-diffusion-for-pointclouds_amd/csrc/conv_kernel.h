@@ -489,7 +489,124 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   }
 
   SDP_T(3);
-  if (a.dact) {
+  if constexpr (SH == 16) {
+    // ------------------------------------------------------------------ epilogue, 16x16 fragments
+    // Register r of fragment (mb, nj) of lane l holds pixel 4 (l / 16) + r of the fragment's 16-px
+    // row segment and Cout 16 nj + l % 16 of the wave's 64: every wave store writes four 64-B runs
+    // of channels.  ConvMeanPool pairs registers r, r+1 (columns) and fragments mb, mb + TC/16
+    // (rows); the 128-pixel InstanceNorm++ group of a channel spans the 4 lanes l % 16 + 16q.
+    __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
+    const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
+    const size_t bo = (size_t)b * Ho * Wo * Cout;
+    const int img_bytes = Ho * Wo * Cout * 4;
+    auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p ? p + bo : a.out + bo), 0, img_bytes, 0x00020000); };
+    const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), o2rs = rs(a.out2), r2rs = rs(a.res2);
+    const int lq = lane >> 4, lcol = lane & 15;
+    constexpr int CB = TC / 16;                      // 16-px fragments per tile row
+    constexpr int NF = POOL ? CB : 8;                // fragments (pooled: row-0 fragments) per lane
+    constexpr int PER = POOL ? 2 : 4;                // values per fragment and lane
+    constexpr int NV = NF * PER;
+    const int xs = (POOL ? 1 : d) * Cout * 4;        // bytes between consecutive output pixels of a run
+    static_for<0, 4>([&](auto njc) {
+      constexpr int nj = decltype(njc)::value;
+      const int co = n0 + wn * 64 + nj * 16 + lcol;
+      const float bias = a.bias ? a.bias[co] : 0.f;
+      int vbase[NF];
+      static_for<0, NF>([&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        if constexpr (POOL) {
+          vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 16) >> 1) + 2 * lq) * Cout + co) * 4;
+        } else {
+          constexpr int mr = f / CB, mc = (f % CB) * 16;
+          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lq) * d + ph_c;
+          vbase[f] = ((y * Wo + x) * Cout + co) * 4;
+        }
+      });
+      float v[NV];
+      if constexpr (POOL) {
+        static_for<0, CB>([&](auto fc) {
+          constexpr int f = decltype(fc)::value;
+          static_for<0, 2>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const float a00 = acc4[f][nj][2 * k], a01 = acc4[f][nj][2 * k + 1];
+            const float a10 = acc4[f + CB][nj][2 * k], a11 = acc4[f + CB][nj][2 * k + 1];
+            v[f * 2 + k] = ((((a00 + bias) + (a10 + bias)) + (a01 + bias)) + (a11 + bias)) / 4.0f;  // layers.py:310-312
+          });
+        });
+      } else {
+        static_for<0, 8>([&](auto fc) {
+          constexpr int f = decltype(fc)::value;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[f * 4 + r] = acc4[f][nj][r] + bias;
+        });
+      }
+      if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor (non-pooled)
+        const int Hi = a.H / 2, Wi = a.W / 2;
+        const float shh = (float)(Hi - 1) / (float)(a.H - 1), sww = (float)(Wi - 1) / (float)(a.W - 1);
+        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const int f = i / PER, k = i % PER;
+          const int mr = f / CB, mc = (f % CB) * 16;
+          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lq + k) * d + ph_c;
+          const float fy = shh * (float)y, fx = sww * (float)x;
+          const int y0 = (int)fy, x0 = (int)fx;
+          const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
+          const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+          const float v00 = ub[((size_t)y0 * Wi + x0) * Cout], v01 = ub[((size_t)y0 * Wi + x0 + xp) * Cout];
+          const float v10 = ub[((size_t)(y0 + yp) * Wi + x0) * Cout];
+          const float v11 = ub[((size_t)(y0 + yp) * Wi + x0 + xp) * Cout];
+          v[i] = v[i] + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
+        }
+      }
+#define SDP_EPI16_OFF(i) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs)
+      if (a.res) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, SDP_EPI16_OFF(i), 0)) + v[i];
+      }
+      if (a.out2) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const float r2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI16_OFF(i), 0));
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2), o2rs, SDP_EPI16_OFF(i), 0);
+        }
+      }
+      if (a.epi_elu) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) v[i] = elu(v[i]);
+      }
+      if constexpr (!(SDP_KO & 16)) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI16_OFF(i), SDP_STORE_AUX);
+      }
+#undef SDP_EPI16_OFF
+      if (a.stats) {
+        float sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sum += v[i];
+        float mean = sum * (1.0f / NV);
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          const float dv = v[i] - mean;
+          m2 = fmaf(dv, dv, m2);
+        }
+        // Chan merges of equal-count partials: lanes l ^ 16 (NV values each), then l ^ 32 (2 NV each)
+        float mp = __shfl_xor(mean, 16), qp = __shfl_xor(m2, 16), dm = mean - mp;
+        m2 = m2 + qp + dm * dm * (0.5f * NV);
+        mean = 0.5f * (mean + mp);
+        mp = __shfl_xor(mean, 32);
+        qp = __shfl_xor(m2, 32);
+        dm = mean - mp;
+        m2 = m2 + qp + dm * dm * (float)NV;
+        mean = 0.5f * (mean + mp);
+        if (lq == 0) {
+          float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile * WM + wm) * Cout + co;
+          *st = make_float2(mean, m2);
+        }
+      }
+    });
+  } else if (a.dact) {
     // data-gradient launches (training): the LDS-staged epilogue -- its 16-B pixel-row
     // accesses of the elu' operand and the residual gradient beat per-channel 4-B accesses
     // ------------------------------------------------------------------ epilogue
