@@ -244,32 +244,49 @@ def run_sampling(args, rank, N, dist, dev):
         merger(x_all, sig[c], setting, 10, 0.01, absmax)
 
     def measure(prec, steps, warmup):
-        """Time `steps` steps with the score net at conv arithmetic `prec`; return (dt, roofline)."""
+        """Time `steps` steps with the score net at conv arithmetic `prec` (profiling OFF), then a
+        separate profiled pass of a few steps for the per-kernel rooflines; return (dt, roofline)."""
         net_box[0] = net if prec == args.precision else ScoreNet(H=H, W=W, precision=prec).load_synthetic()
         cur = net_box[0]
-        cur.profile(True)
-        cur.profile_read()
+        cur.profile(False)
         for i in range(warmup):
             step(i)
-        cur.profile_read()                                  # drop the warmup launches
         dt = timed(step, argparse.Namespace(warmup=0, steps=steps), dist, dev)
+        psteps = min(steps, 5)
+        cur.profile(True)
+        cur.profile_read()
+        for i in range(psteps):
+            step(warmup + steps + i)
+        torch.cuda.synchronize()
         prof = cur.profile_read()
         cur.profile(False)
+        steps = psteps                                  # per-step figures below are over the profiled pass
         if rank == 0:
-            for k, (n_, ms_, fl_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
-                print(f"[conv {prec}] {k:34s} launches {n_:5d} avg {ms_ / n_ * 1e3:8.1f} us  "
-                      f"{fl_ / (ms_ / n_ / 1e3) / 1e12:7.1f} TF/s", file=sys.stderr)
-        cls, (n, ms, fl) = max(prof.items(), key=lambda kv: kv[1][1])
+            for k, (n_, ms_, fl_, by_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+                t_ = ms_ / n_ / 1e3
+                print(f"[{prec}] {k:34s} launches {n_:5d} avg {t_ * 1e6:8.1f} us  {fl_ / t_ / 1e12:7.1f} TF/s  "
+                      f"{by_ / t_ / 1e9:7.1f} GB/s", file=sys.stderr)
+        convs = {k: v for k, v in prof.items() if v[2] > 0}
+        cls, (n, ms, fl, _) = max(convs.items(), key=lambda kv: kv[1][1])
         avg_s = ms / n / 1e3
         achieved = fl / avg_s / 1e12
-        conv_ms = sum(v[1] for v in prof.values()) / steps
+        conv_ms = sum(v[1] for v in convs.values()) / steps
+        # memory-bound kernels of the forward against the HBM roofline (north_star): algorithmic
+        # bytes per launch / average launch time, HIP events on the forward's stream
+        mem = []
+        for k, (n_, ms_, fl_, by_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
+            if fl_ == 0 and by_ > 0:
+                t_ = ms_ / n_ / 1e3
+                mem.append({"kernel": k, "launches_per_step": round(n_ / steps, 2), "avg_launch_us": round(t_ * 1e6, 2),
+                            "algorithmic_bytes": int(by_), "achieved_GBps": round(by_ / t_ / 1e9, 1),
+                            "frac": round(by_ / t_ / 1e9 / HBM_PEAK, 4)})
         traffic, tsrc = pmc_traffic(prec, V, cls) if args.workload == "line" else (None, None)
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[prec], 1),
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK[prec], 4),
                 "traffic": traffic, "traffic_source": tsrc,
                 "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if prec == "bf16" else 4),
                 "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
-                "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3)}
+                "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3), "memory_bound": mem}
         return dt, roof
 
     net_box = [net]

@@ -24,94 +24,145 @@ SDP_DEV float wave_sum(float v) {
 }
 
 // ---------------------------------------------------------------- begin conv (Cin=4 -> 128)
-// block: 64 output pixels of one row x 128 channels; thread = (pixel, 32-channel quarter).
-// The 64 x 128 result goes through LDS so the stores are whole 512-B pixel rows and the
-// per-(b, c) statistics of the 64-pixel tile are a two-pass column sum (no wave shuffles).
+// Persistent; thread = (4 output channels, 16 consecutive pixels) of a 128-pixel row tile.  Its
+// 4 x 36 weights live in registers for the whole launch, so the only LDS traffic is the prepped
+// 4 x 3 x 130 input patch (broadcast b128 reads, 18 values per (channel, row) feed 3 taps x 16 px
+// x 4 channels); the next tile's patch is loaded into registers while the current one computes.
+// Output: every store instruction writes two whole 512-B pixel rows (nt: streamed past L2).
+// Statistics of each 64-pixel half: two-pass (mean, M2) per thread, Chan merges across the
+// 4 pixel groups (lane l ^ 32, then through LDS).  HBM-bound: 8 B in + 512 B out per pixel.
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+constexpr int BC_TP = 128, BC_RS = 132;            // pixels per tile; staged patch row stride (floats)
 __global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ out,
-                                                         float* __restrict__ stats, int H, int W) {
-  constexpr int CO = 128, OS = CO + 4;   // staged row stride (floats)
-  __shared__ float sw[36 * CO];          // [ci*9 + tap][co]
-  __shared__ float sp[4][3][66];         // prepped input patch [ci][row][col]
-  __shared__ float so[64 * OS];          // staged output [px][co]
-  const int tid = threadIdx.x;
-  const int tiles_row = W / 64;
-  const int tiles_per_img = H * tiles_row;
-  const int b = blockIdx.x / tiles_per_img, tile = blockIdx.x % tiles_per_img;
-  const int y = tile / tiles_row, x0 = (tile % tiles_row) * 64;
-  for (int i = tid; i < 36 * CO; i += 256) {
-    const int co = i % CO, k = i / CO;          // k = ci*9 + tap ; w is [co][ci][3][3]
-    sw[i] = w[co * 36 + k];
+                                                         float* __restrict__ stats, int B, int H, int W) {
+  constexpr int CO = 128;
+  __shared__ __attribute__((aligned(16))) float sp[12 * BC_RS];   // [ci*3 + row][col], cols -1 .. 128
+  __shared__ float2 red[2][2][CO];                                   // [64-px half][pixel-group pair][channel]
+  const int tid = threadIdx.x, cg = tid & 31, pg = tid >> 5;       // channels 4cg.., pixels 16pg..
+  f32x2v wr[36][2];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    wr[k][0] = f32x2v{w[(4 * cg + 0) * 36 + k], w[(4 * cg + 1) * 36 + k]};
+    wr[k][1] = f32x2v{w[(4 * cg + 2) * 36 + k], w[(4 * cg + 3) * 36 + k]};
   }
-  for (int i = tid; i < 4 * 3 * 66; i += 256) {
-    const int ci = i / 198, r = (i / 66) % 3, c = i % 66;
-    const int yy = y - 1 + r, xx = x0 - 1 + c;
-    float v = 0.f;
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-      if (ci < 2) v = 2.f * x[(((size_t)b * 2 + ci) * H + yy) * W + xx] - 1.f;
-      else if (ci == 2) v = linspace01(xx, W);
-      else v = linspace01(yy, H);
+  const f32x2v b01 = {bias[4 * cg], bias[4 * cg + 1]}, b23 = {bias[4 * cg + 2], bias[4 * cg + 3]};
+  const int tiles_row = W / BC_TP, tiles_per_img = H * tiles_row, ntiles = B * tiles_per_img;
+  constexpr int PE = (12 * 130 + 255) / 256;
+  auto patch_vals = [&](int t, float (&v)[PE]) {
+    const int b = t / tiles_per_img, tile = t % tiles_per_img;
+    const int y = tile / tiles_row, x0 = (tile % tiles_row) * BC_TP;
+#pragma unroll
+    for (int k = 0; k < PE; ++k) {
+      const int i = tid + k * 256;
+      const int cr = i / 130, c = i % 130, ci = cr / 3, r = cr % 3;
+      const int yy = y - 1 + r, xx = x0 - 1 + c;
+      float e = 0.f;
+      if (i < 12 * 130 && t < ntiles && yy >= 0 && yy < H && xx >= 0 && xx < W) {
+        if (ci < 2) e = 2.f * x[(((size_t)b * 2 + ci) * H + yy) * W + xx] - 1.f;
+        else if (ci == 2) e = linspace01(xx, W);
+        else e = linspace01(yy, H);
+      }
+      v[k] = e;
     }
-    sp[ci][r][c] = v;
-  }
-  __syncthreads();
-  const int px = tid & 63, cq = tid >> 6;
-  float acc[32];
+  };
+  float pv[PE];
+  patch_vals(blockIdx.x, pv);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int b = t / tiles_per_img, tile = t % tiles_per_img;
+    const int y = tile / tiles_row, x0 = (tile % tiles_row) * BC_TP;
+    __syncthreads();                               // the previous tile's patch / red are consumed
 #pragma unroll
-  for (int j = 0; j < 32; ++j) acc[j] = bias[cq * 32 + j];
-  for (int ci = 0; ci < 4; ++ci)
+    for (int k = 0; k < PE; ++k) {
+      const int i = tid + k * 256;
+      if (i < 12 * 130) sp[(i / 130) * BC_RS + i % 130] = pv[k];
+    }
+    __syncthreads();
+    patch_vals(t + gridDim.x, pv);                 // the next tile's patch is in flight meanwhile
+    f32x2v acc[16][2];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      const float v = sp[ci][tap / 3][px + tap % 3];
-      const float* wr = sw + (ci * 9 + tap) * CO + cq * 32;
-#pragma unroll
-      for (int j = 0; j < 32; ++j) acc[j] = fmaf(v, wr[j], acc[j]);
+    for (int i = 0; i < 16; ++i) {
+      acc[i][0] = b01;
+      acc[i][1] = b23;
     }
 #pragma unroll
-  for (int j = 0; j < 32; j += 4)
-    *reinterpret_cast<float4*>(&so[px * OS + cq * 32 + j]) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
-  __syncthreads();
-  // rows: 32 threads per pixel row (16 B each), 8 rows per pass
-  float* o = out + (((size_t)b * H + y) * W + x0) * CO;
-  for (int i = tid; i < 64 * 32; i += 256) {
-    const int p = i >> 5, c4 = i & 31;
-    *reinterpret_cast<float4*>(o + (size_t)p * CO + c4 * 4) = *reinterpret_cast<const float4*>(&so[p * OS + c4 * 4]);
-  }
-  // statistics: thread (channel, half) sums 32 pixels, two passes, Chan merge of the halves
-  const int c = tid & 127, hf = tid >> 7;
-  float sm = 0.f;
-  for (int p = hf * 32; p < hf * 32 + 32; ++p) sm += so[p * OS + c];
-  const float mh = sm * (1.f / 32.f);
-  float m2 = 0.f;
-  for (int p = hf * 32; p < hf * 32 + 32; ++p) {
-    const float dv = so[p * OS + c] - mh;
-    m2 = fmaf(dv, dv, m2);
-  }
-  __syncthreads();
-  float2* red = reinterpret_cast<float2*>(sw);
-  red[tid] = make_float2(mh, m2);
-  __syncthreads();
-  if (hf == 0) {
-    const float2 q = red[tid + 128];
-    const float dm = mh - q.x;
-    float2* st = reinterpret_cast<float2*>(stats) + ((size_t)b * tiles_per_img + tile) * CO + c;
-    *st = make_float2(0.5f * (mh + q.x), m2 + q.y + dm * dm * 16.f);
+    for (int cr = 0; cr < 12; ++cr) {              // (input channel, kernel row)
+      float v[18];
+      const float* row = sp + cr * BC_RS + 16 * pg;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 f = *reinterpret_cast<const float4*>(row + 4 * q);
+        v[4 * q] = f.x; v[4 * q + 1] = f.y; v[4 * q + 2] = f.z; v[4 * q + 3] = f.w;
+      }
+      v[16] = row[16];
+      v[17] = row[17];
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int k = (cr / 3) * 9 + (cr % 3) * 3 + kw;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const f32x2v vv = {v[i + kw], v[i + kw]};
+          acc[i][0] = __builtin_elementwise_fma(vv, wr[k][0], acc[i][0]);
+          acc[i][1] = __builtin_elementwise_fma(vv, wr[k][1], acc[i][1]);
+        }
+      }
+    }
+    float* o = out + (((size_t)b * H + y) * W + x0 + 16 * pg) * CO + 4 * cg;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      __builtin_nontemporal_store(f32x4v{acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y},
+                                  reinterpret_cast<f32x4v*>(o + (size_t)i * CO));
+    // statistics of channel 4cg+j over this thread's 16 pixels, then over 32 (lanes l, l^32 hold
+    // pixel groups 2w, 2w+1), then over 64 (waves 2h, 2h+1 through LDS)
+    float mean[4], m2[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sm += (j & 1) ? acc[i][j >> 1].y : acc[i][j >> 1].x;
+      mean[j] = sm * (1.f / 16.f);
+      float q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float dv = ((j & 1) ? acc[i][j >> 1].y : acc[i][j >> 1].x) - mean[j];
+        q = fmaf(dv, dv, q);
+      }
+      m2[j] = q;
+      const float mp = __shfl_xor(mean[j], 32), qp = __shfl_xor(m2[j], 32), d = mean[j] - mp;
+      m2[j] = m2[j] + qp + d * d * 8.f;
+      mean[j] = 0.5f * (mean[j] + mp);
+    }
+    const int wv = tid >> 6, half = wv >> 1;
+    if ((tid & 63) < 32) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[half][wv & 1][4 * cg + j] = make_float2(mean[j], m2[j]);
+    }
+    __syncthreads();
+    {
+      const int hh = tid >> 7, c = tid & 127;       // 256 threads = 2 halves x 128 channels
+      const float2 a = red[hh][0][c], q = red[hh][1][c];
+      const float d = a.x - q.x;
+      float2* st = reinterpret_cast<float2*>(stats) + ((size_t)b * (H * W / 64) + (y * W + x0) / 64 + hh) * CO + c;
+      *st = make_float2(0.5f * (a.x + q.x), a.y + q.y + d * d * 16.f);
+    }
   }
 }
 
 // ---------------------------------------------------------------- end conv (128 -> 2), NCHW out
 // block: 4 rows x 64 cols of output.  Per 32-channel chunk the (6 x 66) patch (IN++ affine +
-// ELU applied on the way in) sits in LDS; wave g (warp-uniform) takes channels 8g..8g+7 of
-// the chunk, each thread one column: a patch column of 6 rows feeds its 4 output rows x 3
-// taps x 2 channels, so every LDS read serves 4 FMAs.  The 4 channel-group partials are
-// summed through LDS at the end.
+// ELU applied on the way in) sits in LDS at a 36-float pixel stride (16-B aligned, conflict-free
+// ds_read_b128 across consecutive pixels); the NEXT chunk's raw patch is loaded into registers
+// while the current one is consumed.  Wave g takes channels 8g..8g+7 of the chunk, each thread one
+// column: per kw a patch column of 6 rows x 4 channels (6 b128 reads) feeds its 4 output rows x
+// 3 taps x 2 outputs x 4 channels = 96 FMAs.  The 4 channel-group partials are summed through LDS.
+constexpr int EC_PS = 36, EC_NU = (6 * 66 * 8 + 255) / 256;   // pixel stride (floats); units per thread
 __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__ in, const float* __restrict__ ss,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        const float* __restrict__ sigmas, const int64_t* __restrict__ labels,
                                                        float* __restrict__ out, int H, int W, int Cin) {
-  constexpr int PS = 33;
-  __shared__ float sp[6 * 66 * PS];
-  __shared__ float sw[2 * 32 * 9];   // [co][ci][tap] of the chunk
+  __shared__ __attribute__((aligned(16))) float sp[6 * 66 * EC_PS];
+  __shared__ __attribute__((aligned(16))) float sw[2 * 9 * 32];   // [co][tap][ci] of the chunk
   __shared__ float red[4][8][64];
   const int tid = threadIdx.x;
   const int tiles_row = W / 64, tiles_per_img = (H / 4) * tiles_row;
@@ -119,50 +170,75 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
   const int y0 = (tile / tiles_row) * 4, x0 = (tile % tiles_row) * 64;
   const int c = tid & 63, g = tid >> 6;
   const float* ssb = ss + (size_t)b * Cin * 2;
-  float acc[4][2];
+  float4 raw[EC_NU];
+  auto load_chunk = [&](int c0) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = 0.f;
-  for (int c0 = 0; c0 < Cin; c0 += 32) {
-    __syncthreads();
-    for (int i = tid; i < 6 * 66 * 8; i += 256) {
+    for (int k = 0; k < EC_NU; ++k) {
+      const int i = tid + k * 256;
       const int pix = i >> 3, cv = i & 7;
       const int pr = pix / 66, pc = pix % 66;
       const int yy = y0 - 1 + pr, xx = x0 - 1 + pc;
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < 6 * 66 * 8 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+        v = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * Cin + c0 + cv * 4);
+      raw[k] = v;
+    }
+  };
+  float acc[4][2];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = 0.f;
+  load_chunk(0);
+  for (int c0 = 0; c0 < Cin; c0 += 32) {
+    __syncthreads();                                 // the previous chunk's patch is consumed
+#pragma unroll
+    for (int k = 0; k < EC_NU; ++k) {              // transform (zero padding stays zero) -> LDS
+      const int i = tid + k * 256;
+      if (i >= 6 * 66 * 8) break;
+      const int pix = i >> 3, cv = i & 7;
+      const int pr = pix / 66, pc = pix % 66;
+      const int yy = y0 - 1 + pr, xx = x0 - 1 + pc;
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
       if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
         const int ch = c0 + cv * 4;
-        const float4 f = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * Cin + ch);
-        const float fv[4] = {f.x, f.y, f.z, f.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = elu(fmaf(fv[k], ssb[(ch + k) * 2], ssb[(ch + k) * 2 + 1]));
+        const float4 f = raw[k];
+        o.x = elu(fmaf(f.x, ssb[ch * 2], ssb[ch * 2 + 1]));
+        o.y = elu(fmaf(f.y, ssb[(ch + 1) * 2], ssb[(ch + 1) * 2 + 1]));
+        o.z = elu(fmaf(f.z, ssb[(ch + 2) * 2], ssb[(ch + 2) * 2 + 1]));
+        o.w = elu(fmaf(f.w, ssb[(ch + 3) * 2], ssb[(ch + 3) * 2 + 1]));
       }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) sp[pix * PS + cv * 4 + k] = v[k];
+      *reinterpret_cast<float4*>(&sp[pix * EC_PS + cv * 4]) = o;
     }
-    for (int i = tid; i < 2 * 32 * 9; i += 256) {
+    for (int i = tid; i < 2 * 32 * 9; i += 256) {   // w [co][ci][3][3] -> sw [co][tap][ci]
       const int co = i / 288, rem = i % 288, ci = rem / 9, tap = rem % 9;
-      sw[i] = w[((size_t)co * Cin + c0 + ci) * 9 + tap];
+      sw[(co * 9 + tap) * 32 + ci] = w[((size_t)co * Cin + c0 + ci) * 9 + tap];
     }
     __syncthreads();
-    for (int cj = 0; cj < 8; ++cj) {
-      const int ci = g * 8 + cj;
-      float wv[2][9];
+    if (c0 + 32 < Cin) load_chunk(c0 + 32);          // next chunk in flight during this one
 #pragma unroll
-      for (int co = 0; co < 2; ++co)
-#pragma unroll
-        for (int t = 0; t < 9; ++t) wv[co][t] = sw[co * 288 + ci * 9 + t];
+    for (int cq = 0; cq < 2; ++cq) {
+      const int ci = g * 8 + cq * 4;
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
-        float col[6];
+        float4 col[6];
 #pragma unroll
-        for (int pr = 0; pr < 6; ++pr) col[pr] = sp[(pr * 66 + c + kw) * PS + ci];
+        for (int pr = 0; pr < 6; ++pr) col[pr] = *reinterpret_cast<const float4*>(&sp[(pr * 66 + c + kw) * EC_PS + ci]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int kh = 0; kh < 3; ++kh) {
+          const float4 w0 = *reinterpret_cast<const float4*>(&sw[(0 * 9 + kh * 3 + kw) * 32 + ci]);
+          const float4 w1 = *reinterpret_cast<const float4*>(&sw[(1 * 9 + kh * 3 + kw) * 32 + ci]);
 #pragma unroll
-          for (int kh = 0; kh < 3; ++kh) {
-            acc[r][0] = fmaf(col[r + kh], wv[0][kh * 3 + kw], acc[r][0]);
-            acc[r][1] = fmaf(col[r + kh], wv[1][kh * 3 + kw], acc[r][1]);
+          for (int r = 0; r < 4; ++r) {
+            const float4 v = col[r + kh];
+            acc[r][0] = fmaf(v.x, w0.x, acc[r][0]);
+            acc[r][0] = fmaf(v.y, w0.y, acc[r][0]);
+            acc[r][0] = fmaf(v.z, w0.z, acc[r][0]);
+            acc[r][0] = fmaf(v.w, w0.w, acc[r][0]);
+            acc[r][1] = fmaf(v.x, w1.x, acc[r][1]);
+            acc[r][1] = fmaf(v.y, w1.y, acc[r][1]);
+            acc[r][1] = fmaf(v.z, w1.z, acc[r][1]);
+            acc[r][1] = fmaf(v.w, w1.w, acc[r][1]);
           }
+        }
       }
     }
   }
@@ -184,38 +260,42 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
 // ---------------------------------------------------------------- IN++ finalize
 // stats [B][T][C] of float2 (tile mean, tile M2) with `cnt` values per tile -> ss [B][C] of
 // float2 (scale, shift) such that IN++(x) = x*scale + shift.  Two launches:
-//   inpp_moments : one 1024-thread block per (image, 64 channels), 16 tile groups; Chan merge
-//                  of the equal-count partials in float64 -> (mean, biased var) per (b, c)
+//   inpp_moments : B * C/8 blocks of 1024 threads = 8 channels x 128 tile groups; Chan merge of
+//                  the equal-count tile partials in float64, fixed-order tree (deterministic,
+//                  batch invariant) -> (mean, biased var) per (b, c)
 //   inpp_ss      : one block per image over its C channels: m = mean_c(mean), v = unbiased
-//                  var_c(mean) (normalization.py:164-166), then the affine of every channel
-constexpr int INPP_G = 16;   // tile groups (one wave each) per inpp_moments block of 64 channels
-__global__ __launch_bounds__(64 * INPP_G) void inpp_moments_kernel(const float2* __restrict__ stats, int T, float cnt,
-                                                                   int C, double2* __restrict__ mv) {
-  __shared__ double red[64 * INPP_G];
-  const int cb = C / 64, l = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int b = blockIdx.x / cb, c = (blockIdx.x % cb) * 64 + l;
+//                  var_c(mean) (normalization.py:164-166), then the affine of every channel.
+// (One launch with a last-block ticket measured slower: the device-scope fences each block needs
+// to publish its moments across XCDs cost more than the second launch.)
+constexpr int INPP_CPB = 8, INPP_G = 1024 / INPP_CPB;
+__global__ __launch_bounds__(1024) void inpp_moments_kernel(const float2* __restrict__ stats, int T, float cnt, int C,
+                                                            double2* __restrict__ mv) {
+  __shared__ double red[1024];
+  const int tid = threadIdx.x, l = tid % INPP_CPB, g = tid / INPP_CPB;
+  const int nb = C / INPP_CPB;
+  const int b = blockIdx.x / nb, c = (blockIdx.x % nb) * INPP_CPB + l;
   const float2* st = stats + (size_t)b * T * C + c;
-  auto block_sum = [&](double v) {
-    red[threadIdx.x] = v;
+  auto group_sum = [&](double v) {   // sum over the 128 tile groups of each channel, fixed tree order
+    red[tid] = v;
     __syncthreads();
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < INPP_G; ++k) s += red[k * 64 + l];   // fixed order: deterministic
+    for (int s = INPP_G / 2; s > 0; s >>= 1) {
+      if (g < s) red[tid] += red[tid + s * INPP_CPB];
+      __syncthreads();
+    }
+    const double r = red[l];
     __syncthreads();
-    return s;
+    return r;
   };
   double sm = 0.0;
-#pragma unroll 4
   for (int t = g; t < T; t += INPP_G) sm += st[(size_t)t * C].x;
-  const double mean = block_sum(sm) / T;
+  const double mean = group_sum(sm) / T;
   double m2 = 0.0;
-#pragma unroll 4
   for (int t = g; t < T; t += INPP_G) {
     const float2 v = st[(size_t)t * C];
     const double dm = (double)v.x - mean;
     m2 += (double)v.y + dm * dm * cnt;
   }
-  m2 = block_sum(m2);
+  m2 = group_sum(m2);
   if (g == 0) mv[(size_t)b * C + c] = make_double2(mean, m2 / ((double)T * cnt));   // biased (nn.InstanceNorm2d)
 }
 
@@ -253,74 +333,116 @@ __global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict
 }
 
 // ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
-// Separable: a thread owns 4 channels of one column over MP_ROWS output rows; it takes the
-// 5-wide horizontal max of every input row it needs (MP_ROWS + 4 of them) once and slides a
-// 5-row window over them -> 5*(MP_ROWS+4)/MP_ROWS loads per output instead of 25.
+// Block = a strip of MP_COLS columns x 128 channels (32 float4 lanes per pixel, so a wave reads
+// two whole 512-B pixel rows) over MP_ROWS output rows.  Per input row the block lands the strip
+// plus its 2+2 halo columns in LDS ONCE (double-buffered: one barrier per row), every thread takes
+// the 5-wide horizontal max of its (column, 4 channels) from LDS, and slides a 5-row window of
+// those maxima in registers -> per output (MP_COLS+4)/MP_COLS x (MP_ROWS+4)/MP_ROWS global reads
+// instead of 5 x (MP_ROWS+4)/MP_ROWS.
 // idx (training): window position 0..24 of the max in row-major window order, the first one
 // on ties (strict > along the row, then strict > down the rows) -- the index torch's
 // max_pool2d keeps for its backward.  -inf padding never wins.
-constexpr int MP_ROWS = 16;
+constexpr int MP_ROWS = 16, MP_COLS = 8;
 __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                        uchar4* __restrict__ idx, int B, int H, int W, int C) {
-  const int C4 = C / 4, RB = (H + MP_ROWS - 1) / MP_ROWS;
-  const size_t n = (size_t)B * RB * W * C4;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c4 = i % C4;
-    size_t p = i / C4;
-    const int x = p % W;
-    p /= W;
-    const int rb = p % RB;
-    const int b = p / RB;
-    const int y0 = rb * MP_ROWS, y1 = min(H, y0 + MP_ROWS);
-    float4 hm[5];          // horizontal maxima of rows y-2 .. y+2 (ring)
-    uchar4 hc[5];          // their column positions dx+2
-    auto hrow = [&](int yy, float4& m, uchar4& c) {
-      m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-      c = make_uchar4(2, 2, 2, 2);
-      if (yy < 0 || yy >= H) return;
-      const float* row = in + (((size_t)b * H + yy) * W) * C + c4 * 4;
+  constexpr int SC = MP_COLS + 4;                  // staged columns
+  __shared__ float4 row_buf[2][SC * 32];
+  const int tid = threadIdx.x, c4 = tid & 31, xl = tid >> 5;   // (column in strip, float4 channel group)
+  const int C4 = C / 4, CG = C4 / 32;              // 128-channel groups
+  const int strips = W / MP_COLS, RB = (H + MP_ROWS - 1) / MP_ROWS;
+  int t = blockIdx.x;
+  const int cg = t % CG;
+  t /= CG;
+  const int strip = t % strips;
+  t /= strips;
+  const int rb = t % RB, b = t / RB;
+  const int x0 = strip * MP_COLS, y0 = rb * MP_ROWS, y1 = min(H, y0 + MP_ROWS);
+  const int x = x0 + xl;
+  const float NEG = -INFINITY;
+  // input row yy of the strip (+ halo): SC*32 float4 over 256 threads -> at most 2 per thread,
+  // loaded into registers one row ahead of their LDS store (the load latency overlaps a row)
+  constexpr int PT = (SC * 32 + 255) / 256;
+  auto load_row = [&](int yy, float4 (&r)[PT]) {
 #pragma unroll
-      for (int dx = -2; dx <= 2; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= W) continue;
-        const float4 v = *reinterpret_cast<const float4*>(row + (size_t)xx * C);
-        const unsigned char k = (unsigned char)(dx + 2);
-        if (v.x > m.x) { m.x = v.x; c.x = k; }
-        if (v.y > m.y) { m.y = v.y; c.y = k; }
-        if (v.z > m.z) { m.z = v.z; c.z = k; }
-        if (v.w > m.w) { m.w = v.w; c.w = k; }
-      }
-    };
-#pragma unroll
-    for (int k = 0; k < 4; ++k) hrow(y0 - 2 + k, hm[k], hc[k]);
-    for (int y = y0; y < y1; ++y) {
-      hrow(y + 2, hm[4], hc[4]);
-      float4 m = hm[0];
-      uchar4 bi = make_uchar4(hc[0].x, hc[0].y, hc[0].z, hc[0].w);   // row 0 of the window
-#pragma unroll
-      for (int r = 1; r < 5; ++r) {
-        const unsigned char ro = (unsigned char)(5 * r);
-        if (hm[r].x > m.x) { m.x = hm[r].x; bi.x = ro + hc[r].x; }
-        if (hm[r].y > m.y) { m.y = hm[r].y; bi.y = ro + hc[r].y; }
-        if (hm[r].z > m.z) { m.z = hm[r].z; bi.z = ro + hc[r].z; }
-        if (hm[r].w > m.w) { m.w = hm[r].w; bi.w = ro + hc[r].w; }
-      }
-      const size_t o = (((size_t)b * H + y) * W + x) * C4 + c4;
-      reinterpret_cast<float4*>(out)[o] = m;
-      if (idx) idx[o] = bi;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        hm[r] = hm[r + 1];
-        hc[r] = hc[r + 1];
-      }
+    for (int k = 0; k < PT; ++k) {
+      const int i = tid + k * 256;
+      const int sc = i >> 5, cc = i & 31, xx = x0 - 2 + sc;
+      float4 v = make_float4(NEG, NEG, NEG, NEG);
+      if (i < SC * 32 && yy >= 0 && yy < H && xx >= 0 && xx < W)
+        v = reinterpret_cast<const float4*>(in)[(((size_t)b * H + yy) * W + xx) * C4 + cg * 32 + cc];
+      r[k] = v;
     }
+  };
+  auto store_row = [&](int slot, const float4 (&r)[PT]) {
+#pragma unroll
+    for (int k = 0; k < PT; ++k)
+      if (tid + k * 256 < SC * 32) row_buf[slot][tid + k * 256] = r[k];
+  };
+  auto stage = [&](int yy, int slot) {
+    float4 r[PT];
+    load_row(yy, r);
+    store_row(slot, r);
+  };
+  auto hmax = [&](int slot, float4& m, uchar4& c) {
+    m = make_float4(NEG, NEG, NEG, NEG);
+    c = make_uchar4(2, 2, 2, 2);
+#pragma unroll
+    for (int dx = 0; dx < 5; ++dx) {
+      const float4 v = row_buf[slot][(xl + dx) * 32 + c4];
+      const unsigned char k = (unsigned char)dx;
+      if (v.x > m.x) { m.x = v.x; c.x = k; }
+      if (v.y > m.y) { m.y = v.y; c.y = k; }
+      if (v.z > m.z) { m.z = v.z; c.z = k; }
+      if (v.w > m.w) { m.w = v.w; c.w = k; }
+    }
+  };
+  float4 hm[5];
+  uchar4 hc[5];
+  // rows y0-2 .. y0+1 prime the window; row r of the strip sits in slot (r - y0) & 1, staged one
+  // iteration before it is read, so every row costs one barrier
+  stage(y0 - 2, 0);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    stage(y0 - 1 + k, (k + 1) & 1);                // k = 3 stages row y0+2 for the first output row
+    hmax(k & 1, hm[k], hc[k]);
+    __syncthreads();
+  }
+  float4 pre[PT];
+  load_row(y0 + 3, pre);
+  for (int y = y0; y < y1; ++y) {
+    const int slot = (y - y0) & 1;                 // row y+2
+    hmax(slot, hm[4], hc[4]);
+    store_row(slot ^ 1, pre);                      // row y+3, loaded during the previous row
+    load_row(y + 4, pre);
+    float4 m = hm[0];
+    uchar4 bi = hc[0];                             // row 0 of the window
+#pragma unroll
+    for (int r = 1; r < 5; ++r) {
+      const unsigned char ro = (unsigned char)(5 * r);
+      if (hm[r].x > m.x) { m.x = hm[r].x; bi.x = ro + hc[r].x; }
+      if (hm[r].y > m.y) { m.y = hm[r].y; bi.y = ro + hc[r].y; }
+      if (hm[r].z > m.z) { m.z = hm[r].z; bi.z = ro + hc[r].z; }
+      if (hm[r].w > m.w) { m.w = hm[r].w; bi.w = ro + hc[r].w; }
+    }
+    const size_t o = (((size_t)b * H + y) * W + x) * C4 + cg * 32 + c4;
+    reinterpret_cast<float4*>(out)[o] = m;
+    if (idx) idx[o] = bi;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      hm[r] = hm[r + 1];
+      hc[r] = hc[r + 1];
+    }
+    __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------- host launchers
 hipError_t begin_conv(const float* x, const float* w, const float* bias, float* out, float* stats, int B, int H, int W,
                       hipStream_t st) {
-  hipLaunchKernelGGL(begin_conv_kernel, dim3(B * H * (W / 64)), dim3(256), 0, st, x, w, bias, out, stats, H, W);
+  if (W % BC_TP) return hipErrorInvalidValue;
+  const int ntiles = B * H * (W / BC_TP);
+  hipLaunchKernelGGL(begin_conv_kernel, dim3(std::min(ntiles, 512)), dim3(256), 0, st, x, w, bias, out, stats, B, H, W);
   return hipGetLastError();
 }
 
@@ -335,16 +457,16 @@ hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, con
                          const float* beta, float* ss, hipStream_t st, float* nst, void* scratch) {
   if (C % 64 || C > 1024 || (C & (C - 1))) return hipErrorInvalidValue;
   double2* mv = reinterpret_cast<double2*>(scratch);
-  hipLaunchKernelGGL(inpp_moments_kernel, dim3(B * (C / 64)), dim3(64 * INPP_G), 0, st, reinterpret_cast<const float2*>(stats), T,
-                     cnt, C, mv);
+  hipLaunchKernelGGL(inpp_moments_kernel, dim3(B * (C / INPP_CPB)), dim3(1024), 0, st,
+                     reinterpret_cast<const float2*>(stats), T, cnt, C, mv);
   hipLaunchKernelGGL(inpp_ss_kernel, dim3(B), dim3(C), 0, st, mv, C, alpha, gamma, beta, reinterpret_cast<float2*>(ss),
                      reinterpret_cast<float4*>(nst));
   return hipGetLastError();
 }
 
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
-  const size_t n = (size_t)B * ((H + MP_ROWS - 1) / MP_ROWS) * W * (C / 4);
-  const int grid = (int)std::min<size_t>((n + 255) / 256, 256 * 16);
+  if (C % 128 || W % MP_COLS) return hipErrorInvalidValue;
+  const int grid = B * ((H + MP_ROWS - 1) / MP_ROWS) * (W / MP_COLS) * (C / 128);
   hipLaunchKernelGGL(maxpool5_kernel, dim3(grid), dim3(256), 0, st, in, out, reinterpret_cast<uchar4*>(idx), B, H, W, C);
   return hipGetLastError();
 }

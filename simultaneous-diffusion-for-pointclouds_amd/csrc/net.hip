@@ -78,6 +78,7 @@ struct Fwd {
                 std::to_string(out.C) + " @" + std::to_string(in.H) + "x" + std::to_string(in.W) + " d" +
                 std::to_string(o.dil) + (o.pool ? " pool" : "");
       rec.flops = 2.0 * B * in.H * in.W * (double)in.C * out.C * ks * ks;
+      rec.bytes = 4.0 * B * ((double)in.H * in.W * in.C + (double)out.H * out.W * out.C) + 4.0 * out.C * in.C * ks * ks;
       rec.a = net->event();
       rec.b = net->event();
       chk(hipEventRecord(rec.a, st), "hipEventRecord");
@@ -90,11 +91,37 @@ struct Fwd {
     }
   }
 
+  // a non-conv launch under the profiler: class name + algorithmic bytes (HBM roofline)
+  template <class F>
+  void prof_launch(const std::string& cls, double bytes, F&& launch) {
+    sdp_net::ProfRec rec;
+    if (net->profile) {
+      rec.cls = cls;
+      rec.flops = 0;
+      rec.bytes = bytes;
+      rec.a = net->event();
+      rec.b = net->event();
+      chk(hipEventRecord(rec.a, st), "hipEventRecord");
+    }
+    launch();
+    if (net->profile) {
+      chk(hipEventRecord(rec.b, st), "hipEventRecord");
+      net->prof.push_back(rec);
+    }
+  }
+
   // stats (written by the previous conv) -> scale/shift of InstanceNorm2dPlus `nkey`
   void norm(const std::string& nkey, int T, float cnt, int C) {
-    chk(inpp_finalize(stats, B, T, cnt, C, net->P(nkey + ".alpha"), net->P(nkey + ".gamma"), net->P(nkey + ".beta"), ss,
-                      st, nullptr, mv),
-        "inpp_finalize");
+    prof_launch("inpp_finalize C" + std::to_string(C), (double)B * T * C * 8 + (double)B * C * 8, [&] {
+      chk(inpp_finalize(stats, B, T, cnt, C, net->P(nkey + ".alpha"), net->P(nkey + ".gamma"), net->P(nkey + ".beta"),
+                        ss, st, nullptr, mv),
+          "inpp_finalize");
+    });
+  }
+  void pool(const Buf& X, const Buf& P) {
+    const double bytes = 2.0 * B * X.H * X.W * X.C * 4;
+    prof_launch("maxpool5 " + std::to_string(X.C) + " @" + std::to_string(X.H) + "x" + std::to_string(X.W), bytes,
+                [&] { chk(maxpool5(X.p, P.p, B, X.H, X.W, X.C, st), "maxpool5"); });
   }
   static int tiles(const Buf& b) { return b.H * b.W / 128; }
 
@@ -160,13 +187,13 @@ struct Fwd {
   // CRPBlock (layers.py:76-83) on X = ELU(h) (already applied by the producer)
   // -> returns x2 ; slots: P (pool), Q (path), R (x1), S (x2)
   Buf crp(const std::string& k, const Buf& X, const Buf& P, const Buf& Qp, const Buf& R, const Buf& S) {
-    chk(maxpool5(X.p, P.p, B, X.H, X.W, X.C, st), "maxpool5");
+    pool(X, P);
     Opt a;
     a.bias = false;
     a.out2 = R.p;
     a.res2 = X.p;
     conv(P, k + ".convs.0", Qp, a);                   // path1 -> Qp ; x1 = path1 + X -> R
-    chk(maxpool5(Qp.p, P.p, B, X.H, X.W, X.C, st), "maxpool5");
+    pool(Buf{Qp.p, X.H, X.W, X.C}, P);
     Opt b;
     b.bias = false;
     b.res = R.p;
@@ -203,7 +230,11 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
 
   using Opt = Fwd::Opt;
   // begin_conv + input prep  -> FA (stats over 64-px tiles)
-  chk(begin_conv(x, net->P("begin_conv.weight"), net->P("begin_conv.bias"), FA.p, f.stats, B, H, W, st), "begin_conv");
+  f.prof_launch("begin_conv 4->128 @" + std::to_string(H) + "x" + std::to_string(W),
+                (double)B * H * W * (2 * 4 + C * 4) + (double)B * (H * W / 64) * C * 8, [&] {
+                  chk(begin_conv(x, net->P("begin_conv.weight"), net->P("begin_conv.bias"), FA.p, f.stats, B, H, W, st),
+                      "begin_conv");
+                });
   // res1
   f.resblock("res1.0", FA, FB, FD, FC, false, 1, true, H * W / 64, 64.f);
   f.resblock("res1.1", FC, FB, FD, L1, false, 1, true, Fwd::tiles(FC), 128.f);
@@ -261,9 +292,12 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
   Buf o = f.rcu("refine4.output_convs", x2, 3, FA, FB, FD, false, true);           // FB, stats
   // head: IN++ -> ELU -> end_conv -> / sigmas[y]
   f.norm("normalizer", Fwd::tiles(o), 128.f, C);
-  chk(end_conv(o.p, f.ss, net->P("end_conv.weight"), net->P("end_conv.bias"), net->P("sigmas"), labels, out, B, H, W, C,
-               st),
-      "end_conv");
+  f.prof_launch("end_conv 128->2 @" + std::to_string(H) + "x" + std::to_string(W), (double)B * H * W * (C * 4 + 2 * 4),
+                [&] {
+                  chk(end_conv(o.p, f.ss, net->P("end_conv.weight"), net->P("end_conv.bias"), net->P("sigmas"), labels,
+                               out, B, H, W, C, st),
+                      "end_conv");
+                });
 }
 
 static size_t workspace_bytes(const sdp_net* net, int B) {
@@ -437,11 +471,11 @@ int sdp_net_profile_enable(sdp_net* net, int enable) {
 }
 
 // Synchronise on the recorded events and aggregate them per conv class.  Writes up to
-// `cap` rows of "class\tlaunches\ttotal_ms\tflops_per_launch\n" into buf (NUL-terminated)
+// `cap` rows of "class\tlaunches\ttotal_ms\tflops_per_launch\tbytes_per_launch\n" into buf (NUL-terminated)
 // and releases the events.  Returns 0; *n_launches receives the number of launches read.
 int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches) {
   if (!net || !buf || cap == 0) return fail("sdp_net_profile_read: bad argument");
-  struct Agg { int n = 0; double ms = 0, flops = 0; };
+  struct Agg { int n = 0; double ms = 0, flops = 0, bytes = 0; };
   std::map<std::string, Agg> agg;
   try {
     for (auto& r : net->prof) {
@@ -452,6 +486,7 @@ int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches) {
       g.n += 1;
       g.ms += ms;
       g.flops = r.flops;
+      g.bytes = r.bytes;
       net->ev_pool.push_back(r.a);
       net->ev_pool.push_back(r.b);
     }
@@ -463,7 +498,7 @@ int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches) {
   std::string out;
   for (auto& kv : agg)
     out += kv.first + "\t" + std::to_string(kv.second.n) + "\t" + std::to_string(kv.second.ms) + "\t" +
-           std::to_string(kv.second.flops) + "\n";
+           std::to_string(kv.second.flops) + "\t" + std::to_string(kv.second.bytes) + "\n";
   std::strncpy(buf, out.c_str(), cap - 1);
   buf[cap - 1] = 0;
   return 0;

@@ -36,6 +36,7 @@ struct sdp_net {
   struct ProfRec {
     std::string cls;
     double flops;
+    double bytes = 0;               // algorithmic HBM bytes of the launch (memory-bound kernels)
     hipEvent_t a, b;
   };
   sdp_net_desc d;

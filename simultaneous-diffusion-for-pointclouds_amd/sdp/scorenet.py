@@ -97,14 +97,15 @@ class ScoreNet:
         _lib.check(_lib.lib().sdp_net_profile_enable(self._h, 1 if enable else 0), "profile_enable")
 
     def profile_read(self):
-        """{conv class: (launches, total_ms, flops_per_launch)} of the forwards since the last read."""
+        """{launch class: (launches, total_ms, flops_per_launch, algorithmic_bytes_per_launch)} of the
+        forwards since the last read (conv classes and the memory-bound kernels)."""
         buf = _lib.C.create_string_buffer(1 << 16)
         n = _lib.I()
         _lib.check(_lib.lib().sdp_net_profile_read(self._h, buf, len(buf), _lib.C.byref(n)), "profile_read")
         out = {}
         for line in buf.value.decode().splitlines():
-            cls, cnt, ms, fl = line.split("\t")
-            out[cls] = (int(cnt), float(ms), float(fl))
+            cls, cnt, ms, fl, by = line.split("\t")
+            out[cls] = (int(cnt), float(ms), float(fl), float(by))
         return out
 
     def eval(self):
