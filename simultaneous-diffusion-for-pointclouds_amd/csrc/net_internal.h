@@ -55,9 +55,31 @@ struct sdp_net {
   bool train_packs = false;         // keep the dgrad packings current in repack()
   int mode = sdp::MODE_F32X3;
   sdp::TrainPlan* plan = nullptr;   // tape of the last sdp_net_forward_train
+  // forward replays: the launch sequence captured once per (x, out, B, workspace) into a HIP
+  // graph (labels are copied into lab_dev first, so they are not part of the key); a few
+  // entries, least recently used evicted
+  struct GraphEntry {
+    const void* x;
+    void* out;
+    int B;
+    void* ws;
+    hipGraphExec_t exec;
+    unsigned long long used;
+  };
+  std::vector<GraphEntry> graphs;
+  unsigned long long graph_clock = 0;
+  hipStream_t cap_stream = nullptr;
+  int64_t* lab_dev = nullptr;       // [lab_cap] labels of the replayed forwards
+  int lab_cap = 0;
+  void drop_graphs() {
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
+    graphs.clear();
+  }
 
   ~sdp_net() {
     release();
+    if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    if (lab_dev) (void)hipFree(lab_dev);
     for (auto& r : prof) {
       (void)hipEventDestroy(r.a);
       (void)hipEventDestroy(r.b);
@@ -65,6 +87,7 @@ struct sdp_net {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
   }
   void release() {
+    drop_graphs();
     for (auto& kv : dev) {
       const bool in_arena = arena && kv.second >= (void*)arena && kv.second < (void*)(arena + arena_floats);
       if (!in_arena) (void)hipFree(kv.second);
