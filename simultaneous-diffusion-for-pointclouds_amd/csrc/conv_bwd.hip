@@ -6,9 +6,21 @@
 // (conv_kernel.h) run on dy with the "dgrad" weight packing (train_aux.hip pack kernel),
 // without prologue, and with the backward epilogue: *elu'(...) of the forward activation
 // (ConvArgs::dact) and the residual add of the gradient already accumulated for its input.
+#include <cstdlib>
+
 #include "conv_kernel.h"
 
 namespace sdp {
+
+// MFMA shape of the data-gradient launches (conv_kernel.h SH; the LDS-staged epilogue handles
+// both): 16 unless SDP_DGRAD_SHAPE=32
+static int dgrad_shape() {
+  static const int sh = [] {
+    const char* e = getenv("SDP_DGRAD_SHAPE");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return sh;
+}
 
 template <int MODE, int WM, int TC, int KS, bool ZP>
 static hipError_t launch_dgrad_t(ConvArgs a, hipStream_t st) {
@@ -16,7 +28,10 @@ static hipError_t launch_dgrad_t(ConvArgs a, hipStream_t st) {
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
+  if (dgrad_shape() == 16)
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

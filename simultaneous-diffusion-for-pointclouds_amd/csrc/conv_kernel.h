@@ -489,7 +489,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   }
 
   SDP_T(3);
-  if constexpr (SH == 16) {
+  if (SH == 16 && !a.dact) {
     // ------------------------------------------------------------------ epilogue, 16x16 fragments
     // Register r of fragment (mb, nj) of lane l holds pixel 4 (l / 16) + r of the fragment's 16-px
     // row segment and Cout 16 nj + l % 16 of the wave's 64: every wave store writes four 64-B runs
@@ -639,16 +639,33 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     static_for<0, 2>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
       // ---- stage this half's accumulators: wave (wm, wn), fragments mb of the half
-      static_for<0, 2>([&](auto ic) {
-        constexpr int mb = POOL ? (h + 2 * decltype(ic)::value) : (2 * h + decltype(ic)::value);
-        constexpr int q0 = decltype(ic)::value * 32;
-        static_for<0, 2>([&](auto nbc) {
-          constexpr int nb = decltype(nbc)::value;
-          float* dst = stage + (wm * 64 + q0 + 4 * (lane >> 5)) * SROW + wn * 64 + nb * 32 + (lane & 31);
+      if constexpr (SH == 32) {
+        static_for<0, 2>([&](auto ic) {
+          constexpr int mb = POOL ? (h + 2 * decltype(ic)::value) : (2 * h + decltype(ic)::value);
+          constexpr int q0 = decltype(ic)::value * 32;
+          static_for<0, 2>([&](auto nbc) {
+            constexpr int nb = decltype(nbc)::value;
+            float* dst = stage + (wm * 64 + q0 + 4 * (lane >> 5)) * SROW + wn * 64 + nb * 32 + (lane & 31);
   #pragma unroll
-          for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * SROW] = acc[mb][nb][r];
+            for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * SROW] = acc[mb][nb][r];
+          });
         });
-      });
+      } else {
+        // 16x16 fragments 4h .. 4h+3 of the wave hold the same 64 pixels as the 32x32 ones
+        // 2h, 2h+1: fragment i, lane pixel 4 (l / 16) + r is staged pixel q = 16 i + 4 (l / 16) + r
+        // (non-pooled only: the data-gradient launches; a pooled forward never takes this path)
+        if constexpr (!POOL) {
+          static_for<0, 4>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            static_for<0, 4>([&](auto njc) {
+              constexpr int nj = decltype(njc)::value;
+              float* dst = stage + (wm * 64 + 16 * i + 4 * (lane >> 4)) * SROW + wn * 64 + nj * 16 + (lane & 15);
+  #pragma unroll
+              for (int r = 0; r < 4; ++r) dst[r * SROW] = acc4[4 * h + i][nj][r];
+            });
+          });
+        }
+      }
       __syncthreads();
       // ---- row phase: output pixels j = pl, pl + PL, ... of this half
   #pragma unroll 2
