@@ -171,20 +171,25 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
     constexpr int J = decltype(buf)::value;
     if constexpr (SDP_KO & 4) return;
     const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096);
+    // (the lo halves only in fp32x3: MODE_BF16 multiplies the hi parts alone)
     if constexpr (SH == 32) {
       static_for<0, 4>([&](auto q) {
-        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
-        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
-        bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
-        bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+        if constexpr (MODE != MODE_BF16 || (decltype(q)::value & 1) == 0) {
+          const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
+          const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
+          bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+          bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
+        }
       });
     } else {
       static_for<0, 4>([&](auto njc) {
         constexpr int nj = decltype(njc)::value;
         const u32x4 vh = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj], so, 0);
-        const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj] + 16, so, 0);
         bq[J][nj >> 1][2 * (nj & 1)] = make_uint4(vh.x, vh.y, vh.z, vh.w);
-        bq[J][nj >> 1][2 * (nj & 1) + 1] = make_uint4(vl.x, vl.y, vl.z, vl.w);
+        if constexpr (MODE != MODE_BF16) {
+          const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj] + 16, so, 0);
+          bq[J][nj >> 1][2 * (nj & 1) + 1] = make_uint4(vl.x, vl.y, vl.z, vl.w);
+        }
       });
     }
   };
