@@ -24,62 +24,81 @@ SDP_DEV float wave_sum(float v) {
 }
 
 // ---------------------------------------------------------------- begin conv (Cin=4 -> 128)
-// Persistent; thread = (4 output channels, 16 consecutive pixels) of a 128-pixel row tile.  Its
-// 4 x 36 weights live in registers for the whole launch, so the only LDS traffic is the prepped
-// 4 x 3 x 130 input patch (broadcast b128 reads, 18 values per (channel, row) feed 3 taps x 16 px
-// x 4 channels); the next tile's patch is loaded into registers while the current one computes.
+// Persistent; thread = (4 output channels, 16 consecutive pixels) of a 128-pixel row tile.  The
+// 36 x 128 weights are staged in LDS once per workgroup ([tap][4-channel group]: one b128 per tap
+// gives a thread its 4 output channels), so a thread holds only its 64 accumulators and the
+// registers allow 4 workgroups per CU; the prepped 4 x 3 x 130 input patch is broadcast by b128
+// reads (18 values per (channel, row) feed 3 taps x 16 px x 4 channels).  The next tile's patch is
+// loaded into registers while the current one computes, by UNCONDITIONAL loads (clamped address,
+// value selected after): a load under a branch makes the compiler wait vmcnt(0) at the join,
+// which on gfx9 also waits for every output store still in flight.
 // Output: every store instruction writes two whole 512-B pixel rows (nt: streamed past L2).
 // Statistics of each 64-pixel half: two-pass (mean, M2) per thread, Chan merges across the
 // 4 pixel groups (lane l ^ 32, then through LDS).  HBM-bound: 8 B in + 512 B out per pixel.
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int BC_TP = 128, BC_RS = 132;            // pixels per tile; staged patch row stride (floats)
-__global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict__ x, const float* __restrict__ w,
+constexpr int BC_WG_PER_CU = 3;
+__global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ out,
                                                          float* __restrict__ stats, int B, int H, int W) {
   constexpr int CO = 128;
   __shared__ __attribute__((aligned(16))) float sp[12 * BC_RS];   // [ci*3 + row][col], cols -1 .. 128
+  __shared__ __attribute__((aligned(16))) float4 swl[36 * 32];    // [tap][cg]: channels 4cg .. 4cg+3
   __shared__ float2 red[2][2][CO];                                   // [64-px half][pixel-group pair][channel]
+  __shared__ __attribute__((aligned(16))) float rawb[4 * 256];      // DMA landing zone of the next patch
   const int tid = threadIdx.x, cg = tid & 31, pg = tid >> 5;       // channels 4cg.., pixels 16pg..
-  f32x2v wr[36][2];
-#pragma unroll
-  for (int k = 0; k < 36; ++k) {
-    wr[k][0] = f32x2v{w[(4 * cg + 0) * 36 + k], w[(4 * cg + 1) * 36 + k]};
-    wr[k][1] = f32x2v{w[(4 * cg + 2) * 36 + k], w[(4 * cg + 3) * 36 + k]};
+  for (int i = tid; i < 36 * 32; i += 256) {
+    const int k = i >> 5, g4 = i & 31;
+    swl[i] = make_float4(w[(4 * g4 + 0) * 36 + k], w[(4 * g4 + 1) * 36 + k], w[(4 * g4 + 2) * 36 + k],
+                         w[(4 * g4 + 3) * 36 + k]);
   }
   const f32x2v b01 = {bias[4 * cg], bias[4 * cg + 1]}, b23 = {bias[4 * cg + 2], bias[4 * cg + 3]};
   const int tiles_row = W / BC_TP, tiles_per_img = H * tiles_row, ntiles = B * tiles_per_img;
-  constexpr int PE = (12 * 130 + 255) / 256;
-  auto patch_vals = [&](int t, float (&v)[PE]) {
+  // patch rows cr = ci*3 + r: the 2 x 3 x 130 image values of the next tile are landed in rawb by
+  // LDS-DMA (4 B per lane, clamped addresses: no branch, nothing the compiler must wait for) while
+  // the current tile computes; the coordinate rows are computed when the patch is staged.  Unit
+  // i = tid + 256k is landed and later read by the same thread, so it needs only the vmcnt wait:
+  // after the DMA each thread issues exactly 17 stores (16 outputs + 1 statistic), and gfx9's
+  // vector memory ops retire in order, so vmcnt <= 17 means the DMA has landed.
+  constexpr int NI = 6 * 130, PE = (NI + 255) / 256;
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, B * 2 * H * W * 4, 0x00020000);
+  auto patch_dma = [&](int t) {
     const int b = t / tiles_per_img, tile = t % tiles_per_img;
     const int y = tile / tiles_row, x0 = (tile % tiles_row) * BC_TP;
 #pragma unroll
     for (int k = 0; k < PE; ++k) {
-      const int i = tid + k * 256;
+      const int i = min(tid + k * 256, NI - 1);
       const int cr = i / 130, c = i % 130, ci = cr / 3, r = cr % 3;
-      const int yy = y - 1 + r, xx = x0 - 1 + c;
-      float e = 0.f;
-      if (i < 12 * 130 && t < ntiles && yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        if (ci < 2) e = 2.f * x[(((size_t)b * 2 + ci) * H + yy) * W + xx] - 1.f;
-        else if (ci == 2) e = linspace01(xx, W);
-        else e = linspace01(yy, H);
-      }
-      v[k] = e;
+      const int yy = min(max(y - 1 + r, 0), H - 1), xx = min(max(x0 - 1 + c, 0), W - 1);
+      const int off = t < ntiles ? ((((b * 2 + ci) * H + yy) * W + xx) * 4) : 0;
+      const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 4);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xrs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(rawb) + base), 4,
+          off, 0, 0, 0);
     }
   };
-  float pv[PE];
-  patch_vals(blockIdx.x, pv);
+  patch_dma(blockIdx.x);
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const int b = t / tiles_per_img, tile = t % tiles_per_img;
     const int y = tile / tiles_row, x0 = (tile % tiles_row) * BC_TP;
+    if (t == (int)blockIdx.x) __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): no stores behind the first DMA
+    else __builtin_amdgcn_s_waitcnt(0x4f71);                        // vmcnt(17)
     __syncthreads();                               // the previous tile's patch / red are consumed
 #pragma unroll
     for (int k = 0; k < PE; ++k) {
       const int i = tid + k * 256;
-      if (i < 12 * 130) sp[(i / 130) * BC_RS + i % 130] = pv[k];
+      const int cr = i / 130, c = i % 130, r = cr % 3;
+      const int yy = y - 1 + r, xx = x0 - 1 + c;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      if (i < NI) {
+        sp[cr * BC_RS + c] = ok ? 2.f * rawb[i] - 1.f : 0.f;              // channels 0, 1: 2x - 1
+        const float e = cr < 3 ? linspace01(xx, W) : linspace01(yy, H);   // rows 6..11: coordinates
+        sp[(cr + 6) * BC_RS + c] = ok ? e : 0.f;
+      }
     }
     __syncthreads();
-    patch_vals(t + gridDim.x, pv);                 // the next tile's patch is in flight meanwhile
+    patch_dma(t + gridDim.x);                      // the next tile's patch lands meanwhile
     f32x2v acc[16][2];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -100,11 +119,13 @@ __global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw) {
         const int k = (cr / 3) * 9 + (cr % 3) * 3 + kw;
+        const float4 wk = swl[k * 32 + cg];
+        const f32x2v w01 = {wk.x, wk.y}, w23 = {wk.z, wk.w};
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const f32x2v vv = {v[i + kw], v[i + kw]};
-          acc[i][0] = __builtin_elementwise_fma(vv, wr[k][0], acc[i][0]);
-          acc[i][1] = __builtin_elementwise_fma(vv, wr[k][1], acc[i][1]);
+          acc[i][0] = __builtin_elementwise_fma(vv, w01, acc[i][0]);
+          acc[i][1] = __builtin_elementwise_fma(vv, w23, acc[i][1]);
         }
       }
     }
@@ -150,26 +171,30 @@ __global__ __launch_bounds__(256) void begin_conv_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------- end conv (128 -> 2), NCHW out
-// block: 4 rows x 64 cols of output.  Per 32-channel chunk the (6 x 66) patch (IN++ affine +
-// ELU applied on the way in) sits in LDS at a 36-float pixel stride (16-B aligned, conflict-free
-// ds_read_b128 across consecutive pixels); the NEXT chunk's raw patch is loaded into registers
-// while the current one is consumed.  Wave g takes channels 8g..8g+7 of the chunk, each thread one
-// column: per kw a patch column of 6 rows x 4 channels (6 b128 reads) feeds its 4 output rows x
-// 3 taps x 2 outputs x 4 channels = 96 FMAs.  The 4 channel-group partials are summed through LDS.
-constexpr int EC_PS = 36, EC_NU = (6 * 66 * 8 + 255) / 256;   // pixel stride (floats); units per thread
+// block: 4 rows x 64 cols of output.  The image's IN++ (scale, shift) and the 2 x 128 x 9 weights
+// (as (co0, co1) pairs per (tap, channel)) are staged in LDS once.  Per 32-channel chunk the
+// (6 x 66) patch (IN++ affine + ELU applied on the way in) sits in LDS at a 36-float pixel stride
+// (16-B aligned, conflict-free ds_read_b128 across consecutive pixels); the NEXT chunk's raw patch
+// is loaded into registers while the current one is consumed, by unconditional loads (clamped
+// address, zero selected after -- no vmcnt(0) at a branch join).  Wave g takes channels 8g..8g+7
+// of the chunk, each thread one column: per kw a patch column of 6 rows x 4 channels (6 b128
+// reads) feeds its 4 output rows x 3 taps x 4 channels of packed (co0, co1) FMAs -- the same
+// per-output fma order as a scalar loop.  The 4 channel-group partials are summed through LDS.
+constexpr int EC_CIN = 128, EC_PS = 36, EC_NU = (6 * 66 * 8 + 255) / 256;   // pixel stride (floats); units per thread
 __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__ in, const float* __restrict__ ss,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        const float* __restrict__ sigmas, const int64_t* __restrict__ labels,
-                                                       float* __restrict__ out, int H, int W, int Cin) {
+                                                       float* __restrict__ out, int H, int W) {
+  constexpr int Cin = EC_CIN;
   __shared__ __attribute__((aligned(16))) float sp[6 * 66 * EC_PS];
-  __shared__ __attribute__((aligned(16))) float sw[2 * 9 * 32];   // [co][tap][ci] of the chunk
-  __shared__ float red[4][8][64];
+  __shared__ __attribute__((aligned(16))) f32x2v sw[9 * Cin];     // [tap][ci] -> (w[co0], w[co1])
+  __shared__ __attribute__((aligned(16))) float4 sss[Cin / 2];    // (scale, shift) of channels 2j, 2j+1
+  __shared__ f32x2v red[4][4][64];
   const int tid = threadIdx.x;
   const int tiles_row = W / 64, tiles_per_img = (H / 4) * tiles_row;
   const int b = blockIdx.x / tiles_per_img, tile = blockIdx.x % tiles_per_img;
   const int y0 = (tile / tiles_row) * 4, x0 = (tile % tiles_row) * 64;
   const int c = tid & 63, g = tid >> 6;
-  const float* ssb = ss + (size_t)b * Cin * 2;
   float4 raw[EC_NU];
   auto load_chunk = [&](int c0) {
 #pragma unroll
@@ -178,16 +203,19 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
       const int pix = i >> 3, cv = i & 7;
       const int pr = pix / 66, pc = pix % 66;
       const int yy = y0 - 1 + pr, xx = x0 - 1 + pc;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (i < 6 * 66 * 8 && yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = *reinterpret_cast<const float4*>(in + (((size_t)b * H + yy) * W + xx) * Cin + c0 + cv * 4);
-      raw[k] = v;
+      const bool ok = i < 6 * 66 * 8 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      raw[k] = *reinterpret_cast<const float4*>(in + (ok ? (((size_t)b * H + yy) * W + xx) * Cin + c0 + cv * 4 : 0));
     }
   };
-  float acc[4][2];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = 0.f;
   load_chunk(0);
+  for (int i = tid; i < 9 * Cin; i += 256) {
+    const int tap = i / Cin, ci = i % Cin;
+    sw[i] = f32x2v{w[(size_t)ci * 9 + tap], w[((size_t)Cin + ci) * 9 + tap]};
+  }
+  if (tid < Cin / 2) sss[tid] = reinterpret_cast<const float4*>(ss + (size_t)b * Cin * 2)[tid];
+  f32x2v acc[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = f32x2v{0.f, 0.f};
   for (int c0 = 0; c0 < Cin; c0 += 32) {
     __syncthreads();                                 // the previous chunk's patch is consumed
 #pragma unroll
@@ -199,18 +227,15 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
       const int yy = y0 - 1 + pr, xx = x0 - 1 + pc;
       float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
       if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        const int ch = c0 + cv * 4;
+        const int j = (c0 + cv * 4) >> 1;
+        const float4 s01 = sss[j], s23 = sss[j + 1];
         const float4 f = raw[k];
-        o.x = elu(fmaf(f.x, ssb[ch * 2], ssb[ch * 2 + 1]));
-        o.y = elu(fmaf(f.y, ssb[(ch + 1) * 2], ssb[(ch + 1) * 2 + 1]));
-        o.z = elu(fmaf(f.z, ssb[(ch + 2) * 2], ssb[(ch + 2) * 2 + 1]));
-        o.w = elu(fmaf(f.w, ssb[(ch + 3) * 2], ssb[(ch + 3) * 2 + 1]));
+        o.x = elu(fmaf(f.x, s01.x, s01.y));
+        o.y = elu(fmaf(f.y, s01.z, s01.w));
+        o.z = elu(fmaf(f.z, s23.x, s23.y));
+        o.w = elu(fmaf(f.w, s23.z, s23.w));
       }
       *reinterpret_cast<float4*>(&sp[pix * EC_PS + cv * 4]) = o;
-    }
-    for (int i = tid; i < 2 * 32 * 9; i += 256) {   // w [co][ci][3][3] -> sw [co][tap][ci]
-      const int co = i / 288, rem = i % 288, ci = rem / 9, tap = rem % 9;
-      sw[(co * 9 + tap) * 32 + ci] = w[((size_t)co * Cin + c0 + ci) * 9 + tap];
     }
     __syncthreads();
     if (c0 + 32 < Cin) load_chunk(c0 + 32);          // next chunk in flight during this one
@@ -224,35 +249,27 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
         for (int pr = 0; pr < 6; ++pr) col[pr] = *reinterpret_cast<const float4*>(&sp[(pr * 66 + c + kw) * EC_PS + ci]);
 #pragma unroll
         for (int kh = 0; kh < 3; ++kh) {
-          const float4 w0 = *reinterpret_cast<const float4*>(&sw[(0 * 9 + kh * 3 + kw) * 32 + ci]);
-          const float4 w1 = *reinterpret_cast<const float4*>(&sw[(1 * 9 + kh * 3 + kw) * 32 + ci]);
+          const f32x2v* wt = &sw[(kh * 3 + kw) * Cin + c0 + ci];
+          const f32x2v w0 = wt[0], w1 = wt[1], w2 = wt[2], w3 = wt[3];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float4 v = col[r + kh];
-            acc[r][0] = fmaf(v.x, w0.x, acc[r][0]);
-            acc[r][0] = fmaf(v.y, w0.y, acc[r][0]);
-            acc[r][0] = fmaf(v.z, w0.z, acc[r][0]);
-            acc[r][0] = fmaf(v.w, w0.w, acc[r][0]);
-            acc[r][1] = fmaf(v.x, w1.x, acc[r][1]);
-            acc[r][1] = fmaf(v.y, w1.y, acc[r][1]);
-            acc[r][1] = fmaf(v.z, w1.z, acc[r][1]);
-            acc[r][1] = fmaf(v.w, w1.w, acc[r][1]);
+            acc[r] = __builtin_elementwise_fma(f32x2v{v.x, v.x}, w0, acc[r]);
+            acc[r] = __builtin_elementwise_fma(f32x2v{v.y, v.y}, w1, acc[r]);
+            acc[r] = __builtin_elementwise_fma(f32x2v{v.z, v.z}, w2, acc[r]);
+            acc[r] = __builtin_elementwise_fma(f32x2v{v.w, v.w}, w3, acc[r]);
           }
         }
       }
     }
   }
-  __syncthreads();
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    red[g][2 * r][c] = acc[r][0];
-    red[g][2 * r + 1][c] = acc[r][1];
-  }
+  for (int r = 0; r < 4; ++r) red[g][r][c] = acc[r];
   __syncthreads();
   const float sg = sigmas[labels[b]];
   for (int i = tid; i < 8 * 64; i += 256) {
     const int k = i >> 6, cc = i & 63, r = k >> 1, co = k & 1;
-    const float v = ((red[0][k][cc] + red[1][k][cc]) + red[2][k][cc]) + red[3][k][cc];
+    const float v = ((red[0][r][cc][co] + red[1][r][cc][co]) + red[2][r][cc][co]) + red[3][r][cc][co];
     out[(((size_t)b * 2 + co) * H + y0 + r) * W + x0 + cc] = (v + bias[co]) / sg;
   }
 }
@@ -334,20 +351,30 @@ __global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict
 
 // ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
 // Block = a strip of MP_COLS columns x 128 channels (32 float4 lanes per pixel, so a wave reads
-// two whole 512-B pixel rows) over MP_ROWS output rows.  Per input row the block lands the strip
-// plus its 2+2 halo columns in LDS ONCE (double-buffered: one barrier per row), every thread takes
-// the 5-wide horizontal max of its (column, 4 channels) from LDS, and slides a 5-row window of
-// those maxima in registers -> per output (MP_COLS+4)/MP_COLS x (MP_ROWS+4)/MP_ROWS global reads
-// instead of 5 x (MP_ROWS+4)/MP_ROWS.
+// two whole 512-B pixel rows) over MP_ROWS output rows.  Each input row of the strip plus its 2+2
+// halo columns is landed in LDS ONCE by LDS-DMA, MP_D rows ahead of its use in a ring of MP_NS
+// row slots; every thread takes the 5-wide horizontal max of its (column, 4 channels) from LDS and
+// slides a 5-row window of those maxima in registers -> per output (MP_COLS+4)/MP_COLS x
+// (MP_ROWS+4)/MP_ROWS global reads.  One barrier per row.  The DMA has no register result, so the
+// compiler places no wait for it: each thread waits for its own DMA of a row with an explicit
+// vmcnt (vector memory ops retire in order on gfx9, and exactly P DMAs + S stores per row follow).
+// Out-of-image rows/columns are read at the clamped (edge) position: a copy of a value that is
+// inside the same 5x5 window, so the max is the one -inf padding gives.
 // idx (training): window position 0..24 of the max in row-major window order, the first one
 // on ties (strict > along the row, then strict > down the rows) -- the index torch's
-// max_pool2d keeps for its backward.  -inf padding never wins.
-constexpr int MP_ROWS = 16, MP_COLS = 8;
+// max_pool2d keeps for its backward.  For it the edge copies are overwritten with -inf (an edge
+// copy sits earlier in window order than its original and would take the tie), so -inf padding
+// never wins.
+constexpr int MP_ROWS = 16, MP_COLS = 8, MP_NS = 8, MP_D = 4;
+template <bool IDX>
 __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                        uchar4* __restrict__ idx, int B, int H, int W, int C) {
   constexpr int SC = MP_COLS + 4;                  // staged columns
-  __shared__ float4 row_buf[2][SC * 32];
+  constexpr int NUNIT = SC * 32;                   // float4 units per staged row: 384 = waves 0..3 + waves 0..1
+  static_assert(NUNIT == 384 && MP_NS >= MP_D + 1 && 4 + MP_D <= MP_NS, "maxpool5 ring layout");
+  __shared__ __attribute__((aligned(16))) float4 row_buf[MP_NS][NUNIT];
   const int tid = threadIdx.x, c4 = tid & 31, xl = tid >> 5;   // (column in strip, float4 channel group)
+  const int wave = tid >> 6;
   const int C4 = C / 4, CG = C4 / 32;              // 128-channel groups
   const int strips = W / MP_COLS, RB = (H + MP_ROWS - 1) / MP_ROWS;
   int t = blockIdx.x;
@@ -359,29 +386,32 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
   const int x0 = strip * MP_COLS, y0 = rb * MP_ROWS, y1 = min(H, y0 + MP_ROWS);
   const int x = x0 + xl;
   const float NEG = -INFINITY;
-  // input row yy of the strip (+ halo): SC*32 float4 over 256 threads -> at most 2 per thread,
-  // loaded into registers one row ahead of their LDS store (the load latency overlaps a row)
-  constexpr int PT = (SC * 32 + 255) / 256;
-  auto load_row = [&](int yy, float4 (&r)[PT]) {
+  const i32x4 rs = buffer_desc(in + (size_t)b * H * W * C, (uint32_t)H * W * C * 4);
+  const uint32_t ring = (uint32_t)reinterpret_cast<uintptr_t>(&row_buf[0][0]);
+  // unit k of this thread: i = tid + 256k (k = 1 only on waves 0, 1), staged column i >> 5
+  int colo[2];
+  bool colok[2];
 #pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      const int i = tid + k * 256;
-      const int sc = i >> 5, cc = i & 31, xx = x0 - 2 + sc;
-      float4 v = make_float4(NEG, NEG, NEG, NEG);
-      if (i < SC * 32 && yy >= 0 && yy < H && xx >= 0 && xx < W)
-        v = reinterpret_cast<const float4*>(in)[(((size_t)b * H + yy) * W + xx) * C4 + cg * 32 + cc];
-      r[k] = v;
+  for (int k = 0; k < 2; ++k) {
+    const int i = tid + k * 256, xx = x0 - 2 + (i >> 5);
+    colok[k] = xx >= 0 && xx < W;
+    colo[k] = ((min(max(xx, 0), W - 1) * C4) + cg * 32 + (i & 31)) * 16;
+  }
+  auto dma_row = [&](int yy, int slot) {
+    const int rowo = min(max(yy, 0), H - 1) * W * C4 * 16;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && wave >= 2) break;              // wave-uniform: units 256..383 are waves 0, 1
+      dma16_lds_opaque(rs, ring + (slot * NUNIT + (tid & ~63) + k * 256) * 16, colo[k], rowo);
     }
   };
-  auto store_row = [&](int slot, const float4 (&r)[PT]) {
+  auto pad_row = [&](int yy, int slot) {           // IDX: the edge copies of this thread's units -> -inf
+    if constexpr (IDX) {
+      const bool rowok = yy >= 0 && yy < H;
 #pragma unroll
-    for (int k = 0; k < PT; ++k)
-      if (tid + k * 256 < SC * 32) row_buf[slot][tid + k * 256] = r[k];
-  };
-  auto stage = [&](int yy, int slot) {
-    float4 r[PT];
-    load_row(yy, r);
-    store_row(slot, r);
+      for (int k = 0; k < 2; ++k)
+        if ((k == 0 || wave < 2) && !(rowok && colok[k])) row_buf[slot][tid + k * 256] = make_float4(NEG, NEG, NEG, NEG);
+    }
   };
   auto hmax = [&](int slot, float4& m, uchar4& c) {
     m = make_float4(NEG, NEG, NEG, NEG);
@@ -398,23 +428,31 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
   };
   float4 hm[5];
   uchar4 hc[5];
-  // rows y0-2 .. y0+1 prime the window; row r of the strip sits in slot (r - y0) & 1, staged one
-  // iteration before it is read, so every row costs one barrier
-  stage(y0 - 2, 0);
+  // row y0 - 2 + ri sits in slot ri % MP_NS.  Prologue: rows ri = 0 .. 3 + MP_D in flight at once;
+  // rows 0..3 prime the window
+#pragma unroll
+  for (int ri = 0; ri < 4 + MP_D; ++ri) dma_row(y0 - 2 + ri, ri);
+  __builtin_amdgcn_s_waitcnt(0x0f70);              // vmcnt(0)
+#pragma unroll
+  for (int ri = 0; ri < 4 + MP_D; ++ri) pad_row(y0 - 2 + ri, ri);
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    stage(y0 - 1 + k, (k + 1) & 1);                // k = 3 stages row y0+2 for the first output row
-    hmax(k & 1, hm[k], hc[k]);
-    __syncthreads();
-  }
-  float4 pre[PT];
-  load_row(y0 + 3, pre);
+  for (int k = 0; k < 4; ++k) hmax(k, hm[k], hc[k]);
+  // iteration j (output row y0 + j) reads row ri = j + 4 and lands row ri = j + 4 + MP_D.  Row
+  // j + 4 was landed at iteration j - MP_D (or in the prologue); after that DMA this thread issued
+  // S stores, then P DMAs + S stores in each of the MP_D - 1 iterations between
+  constexpr int S = IDX ? 2 : 1;
+  constexpr int WAIT01 = S + (MP_D - 1) * (2 + S), WAIT23 = S + (MP_D - 1) * (1 + S);
+  static_assert(WAIT01 < 64, "vmcnt field");
   for (int y = y0; y < y1; ++y) {
-    const int slot = (y - y0) & 1;                 // row y+2
+    const int j = y - y0;
+    const int slot = (j + 4) % MP_NS;
+    if (wave < 2) __builtin_amdgcn_s_waitcnt(0x0f70 | (WAIT01 & 15) | ((WAIT01 >> 4) << 14));
+    else __builtin_amdgcn_s_waitcnt(0x0f70 | (WAIT23 & 15) | ((WAIT23 >> 4) << 14));
+    if (j >= 4) pad_row(y + 2, slot);
+    __syncthreads();                               // row y+2 landed everywhere; row j+4+MP_D-MP_NS consumed
     hmax(slot, hm[4], hc[4]);
-    store_row(slot ^ 1, pre);                      // row y+3, loaded during the previous row
-    load_row(y + 4, pre);
+    dma_row(y + 2 + MP_D, (j + 4 + MP_D) % MP_NS);
     float4 m = hm[0];
     uchar4 bi = hc[0];                             // row 0 of the window
 #pragma unroll
@@ -427,14 +465,14 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
     }
     const size_t o = (((size_t)b * H + y) * W + x) * C4 + cg * 32 + c4;
     reinterpret_cast<float4*>(out)[o] = m;
-    if (idx) idx[o] = bi;
+    if constexpr (IDX) idx[o] = bi;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       hm[r] = hm[r + 1];
       hc[r] = hc[r + 1];
     }
-    __syncthreads();
   }
+  __builtin_amdgcn_s_waitcnt(0x0f70);              // the rows landed past the strip's end
 }
 
 // ---------------------------------------------------------------- host launchers
@@ -442,14 +480,16 @@ hipError_t begin_conv(const float* x, const float* w, const float* bias, float* 
                       hipStream_t st) {
   if (W % BC_TP) return hipErrorInvalidValue;
   const int ntiles = B * H * (W / BC_TP);
-  hipLaunchKernelGGL(begin_conv_kernel, dim3(std::min(ntiles, 512)), dim3(256), 0, st, x, w, bias, out, stats, B, H, W);
+  hipLaunchKernelGGL(begin_conv_kernel, dim3(std::min(ntiles, 256 * BC_WG_PER_CU)), dim3(256), 0, st, x, w, bias, out,
+                     stats, B, H, W);
   return hipGetLastError();
 }
 
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st) {
+  if (Cin != EC_CIN || H % 4 || W % 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(end_conv_kernel, dim3(B * (H / 4) * (W / 64)), dim3(256), 0, st, in, ss, w, bias, sigmas, labels,
-                     out, H, W, Cin);
+                     out, H, W);
   return hipGetLastError();
 }
 
@@ -467,7 +507,11 @@ hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, con
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
   if (C % 128 || W % MP_COLS) return hipErrorInvalidValue;
   const int grid = B * ((H + MP_ROWS - 1) / MP_ROWS) * (W / MP_COLS) * (C / 128);
-  hipLaunchKernelGGL(maxpool5_kernel, dim3(grid), dim3(256), 0, st, in, out, reinterpret_cast<uchar4*>(idx), B, H, W, C);
+  if (idx)
+    hipLaunchKernelGGL(maxpool5_kernel<true>, dim3(grid), dim3(256), 0, st, in, out, reinterpret_cast<uchar4*>(idx), B, H,
+                       W, C);
+  else
+    hipLaunchKernelGGL(maxpool5_kernel<false>, dim3(grid), dim3(256), 0, st, in, out, nullptr, B, H, W, C);
   return hipGetLastError();
 }
 

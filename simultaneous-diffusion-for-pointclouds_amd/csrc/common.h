@@ -28,6 +28,25 @@ enum { MODE_F32 = 0, MODE_F32X3 = 1, MODE_BF16 = 2 };
 enum { PRO_NONE = 0, PRO_ELU = 1, PRO_AFFINE_ELU = 2 };
 
 // nn.ELU(alpha=1) (LiDARGen/models/layers.py:11-13)
+// LDS-DMA of 16 B per lane (lane i lands at lds_byte + 16 i) issued as inline asm, so the compiler
+// does not see it as an LDS write: it inserts no wait for it before later LDS reads (through one
+// shared array it cannot tell the ring slots apart and would wait for every DMA in flight).  The
+// caller waits for it with an explicit s_waitcnt vmcnt.  rsrc: a wave-uniform buffer descriptor
+// (words: base lo, base hi, num_records, 0x00020000).
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+SDP_DEV i32x4 buffer_desc(const void* base, uint32_t bytes) {
+  const uint64_t p = reinterpret_cast<uint64_t>(base);
+  return i32x4{__builtin_amdgcn_readfirstlane((int)(uint32_t)p), __builtin_amdgcn_readfirstlane((int)((p >> 32) & 0xffff)),
+               __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+SDP_DEV void dma16_lds_opaque(i32x4 rsrc, uint32_t lds_byte, int voff, int soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane((int)lds_byte)), "v"(voff), "s"(rsrc),
+                 "s"(__builtin_amdgcn_readfirstlane(soff))
+               : "memory");   // m0 is reserved (not a clobber): nothing else in these kernels uses it
+}
+
 SDP_DEV float elu(float x) { return x > 0.f ? x : (__expf(x) - 1.0f); }
 // the same values without a compare/select (e^x - 1 >= x, and e^min(x,0) - 1 = 0 for x > 0):
 // no VCC round trip, so it schedules freely between MFMAs
