@@ -76,6 +76,9 @@ def parse():
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the world it saw")
     ap.add_argument("--no-fp32-line", action="store_true",
                     help="skip the exact-fp32 (v_mfma_f32_32x32x2_f32) companion measurement of the line workload")
+    ap.add_argument("--unfused", action="store_true",
+                    help="line/allforone: score net and Langevin update as two calls (sdp_net_forward + "
+                         "sdp_langevin_step) instead of sdp_net_forward_langevin")
     ap.add_argument("--cpu-threads", type=int, default=16)
     a = ap.parse_args()
     if a.views is None:
@@ -143,19 +146,22 @@ def pmc_traffic(precision, V, cls):
     """HBM bytes per launch of the dominant conv class, read from the committed PMC passes
     (tools/pmc_traffic.sh -> profiles/r02_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
     correction) + TCC_EA0_WRREQ bytes per launch of that kernel at this grid).  PMC counters cannot
-    be read inside this process, so the value is tagged with the file's source hash: when it does
-    not match the current csrc tree the traffic is reported as null (stale), never as current."""
+    be read inside this process, so the value is tagged with the hash of the conv kernel's sources
+    (sdp/_build.py conv_source_hash: common.h, conv_kernel.h, conv.hip -- what tools/conv_bench is
+    built from): when it does not match the current tree the traffic is reported as null (stale),
+    never as current."""
     try:
         with open(TRAFFIC_FILE) as f:
             doc = json.load(f)
     except OSError:
         return None, None
     from sdp import _build
-    if doc.get("source_hash") != _build.source_hash():
-        return None, f"stale: {os.path.basename(TRAFFIC_FILE)} was measured on another csrc tree"
+    if doc.get("conv_source_hash") != _build.conv_source_hash():
+        return None, f"stale: {os.path.basename(TRAFFIC_FILE)} was measured on another conv kernel source"
     for r in doc.get("rows", []):
         if r.get("precision") == precision and r.get("views") == V and r.get("class") == cls:
-            return round(r["hbm_bytes"]), f"{os.path.basename(TRAFFIC_FILE)} (PMC, source {doc['source_hash'][:12]})"
+            return round(r["hbm_bytes"]), (f"{os.path.basename(TRAFFIC_FILE)} (PMC, conv source "
+                                           f"{doc['conv_source_hash'][:12]})")
     return None, None
 
 
@@ -230,12 +236,16 @@ def run_sampling(args, rank, N, dist, dev):
         c = 2 + (i % (len(sig) - 2))          # levels >= minStepToShare: the merge always runs
         s = np.float32(6.2e-6) * (sig[c] / sig[-1]) ** 2
         ns = np.float32(np.sqrt(np.float32(s * np.float32(2))))
-        net_box[0](x, labels[c], out=grad)
+        seed = 1234 + (rank if args.mode == "megabatch" else 0)
         absmax.zero_()
-        _lib.check(L.sdp_langevin_step(x.data_ptr(), grad.data_ptr(), ref.data_ptr(), mask.data_ptr(), None,
-                                       1234 + (rank if args.mode == "megabatch" else 0), offset[0], float(s),
-                                       float(ns), 1.0, 1, V, 2, H * W, lik.data_ptr(), absmax.data_ptr(), st),
-                   "langevin")
+        if args.unfused:
+            net_box[0](x, labels[c], out=grad)
+            _lib.check(L.sdp_langevin_step(x.data_ptr(), grad.data_ptr(), ref.data_ptr(), mask.data_ptr(), None, seed,
+                                           offset[0], float(s), float(ns), 1.0, 1, V, 2, H * W, lik.data_ptr(),
+                                           absmax.data_ptr(), st), "langevin")
+        else:   # the update in the net's last kernel (sdp_net_forward_langevin), as sdp.sampling runs it
+            net_box[0].forward_langevin(x, labels[c], ref, mask, None, seed, offset[0], float(s), float(ns), 1.0, True,
+                                        lik, absmax)
         offset[0] += n_src * per_view4
         if dist:
             if args.mode == "viewsplit":

@@ -12,6 +12,7 @@
  *   sdp_net_*              scorenet(x, y) = NCSN_LiDAR_small.forward   models/ncsnv2.py:420-518
  *                          weight load    load_state_dict + EMAHelper  runners/ncsn_runner_kitti_simultaneous.py:472-489
  *   sdp_langevin_step      Langevin update                           models/KITTISampling.py:133-156,
+ *   sdp_net_forward_langevin  scorenet + Langevin update in one call   models/KITTISampling.py:137-156
  *                                                                     models/__init__.py:236-259, :1397-1416
  *   sdp_consistency_merge  cross-view reprojection + correction      models/KITTISampling.py:160-490 (pose matrices),
  *                                                                     models/__init__.py:263-579 (origin offsets)
@@ -70,6 +71,25 @@ int sdp_net_workspace_size(const sdp_net* net, int B, size_t* bytes);
 int sdp_net_forward(sdp_net* net, const float* x, const int64_t* labels, float* out, int B,
                     void* workspace, size_t workspace_bytes, void* stream);
 int sdp_net_destroy(sdp_net* net);
+/* One annealed-Langevin step with the update fused into the score net's last kernel
+ * (KITTISampling.py:137-156 in one call): grad = scorenet(x, labels) is computed and, in the same
+ * epilogue, x <- x + step*g' + grad_ref*lik + noise*noise_scale exactly as sdp_langevin_step
+ * (same float32 order, same Philox counters: bit-identical to sdp_net_forward followed by
+ * sdp_langevin_step).  x [B,2,H,W] is read by the first layer and updated in place by the last.
+ * grad_out (nullable) receives the scores; lik_out / absmax_bits as in sdp_langevin_step.     */
+typedef struct {
+  const float* ref;            /* [B,2,H,W] */
+  const int32_t* mask;         /* [B,2,H,W] */
+  const float* noise;          /* nullable: Philox4x32-10(seed, offset + i/4) */
+  uint64_t seed, offset;
+  float step_size, noise_scale, grad_ref;
+  int nan_to_num;
+  float* lik_out;              /* nullable */
+  uint32_t* absmax_bits;       /* nullable */
+  float* grad_out;             /* nullable */
+} sdp_langevin_params;
+int sdp_net_forward_langevin(sdp_net* net, float* x, const int64_t* labels, int B, const sdp_langevin_params* params,
+                             void* workspace, size_t workspace_bytes, void* stream);
 /* Measurement hooks: when enabled, every conv launch of sdp_net_forward is bracketed by HIP
  * events on the forward's stream; sdp_net_profile_read synchronises on them and writes one
  * line per conv class: "class\tlaunches\ttotal_ms\tflops_per_launch\n". */

@@ -7,6 +7,7 @@
 //                (normalization.py:163-176), in two small launches.
 //   maxpool5   : MaxPool2d(5, stride 1, padding 2) of CRPBlock (layers.py:70), NHWC.
 #include "common.h"
+#include "langevin.h"
 
 namespace sdp {
 
@@ -180,11 +181,15 @@ __global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const flo
 // of the chunk, each thread one column: per kw a patch column of 6 rows x 4 channels (6 b128
 // reads) feeds its 4 output rows x 3 taps x 4 channels of packed (co0, co1) FMAs -- the same
 // per-output fma order as a scalar loop.  The 4 channel-group partials are summed through LDS.
+// LGV: the Langevin update of sdp_net_forward_langevin in the epilogue (langevin.h): the block's
+// 4 x 64 x 2 scores update x in place, write lik (and the scores when out is given) and feed
+// max|x_new[:,0]|; the float4 groups are those of the stand-alone kernel, so are the Philox counters.
 constexpr int EC_CIN = 128, EC_PS = 36, EC_NU = (6 * 66 * 8 + 255) / 256;   // pixel stride (floats); units per thread
+template <bool LGV>
 __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__ in, const float* __restrict__ ss,
                                                        const float* __restrict__ w, const float* __restrict__ bias,
                                                        const float* __restrict__ sigmas, const int64_t* __restrict__ labels,
-                                                       float* __restrict__ out, int H, int W) {
+                                                       float* __restrict__ out, int H, int W, LangevinArgs lg) {
   constexpr int Cin = EC_CIN;
   __shared__ __attribute__((aligned(16))) float sp[6 * 66 * EC_PS];
   __shared__ __attribute__((aligned(16))) f32x2v sw[9 * Cin];     // [tap][ci] -> (w[co0], w[co1])
@@ -267,10 +272,32 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
   for (int r = 0; r < 4; ++r) red[g][r][c] = acc[r];
   __syncthreads();
   const float sg = sigmas[labels[b]];
-  for (int i = tid; i < 8 * 64; i += 256) {
-    const int k = i >> 6, cc = i & 63, r = k >> 1, co = k & 1;
-    const float v = ((red[0][r][cc][co] + red[1][r][cc][co]) + red[2][r][cc][co]) + red[3][r][cc][co];
-    out[(((size_t)b * 2 + co) * H + y0 + r) * W + x0 + cc] = (v + bias[co]) / sg;
+  if constexpr (!LGV) {
+    for (int i = tid; i < 8 * 64; i += 256) {
+      const int k = i >> 6, cc = i & 63, r = k >> 1, co = k & 1;
+      const float v = ((red[0][r][cc][co] + red[1][r][cc][co]) + red[2][r][cc][co]) + red[3][r][cc][co];
+      out[(((size_t)b * 2 + co) * H + y0 + r) * W + x0 + cc] = (v + bias[co]) / sg;
+    }
+  } else {
+    uint32_t lmax = 0u;
+    if (tid < 128) {                                 // (row, channel) x 16 float4 groups of 4 columns
+      const int k = tid >> 4, r = k >> 1, co = k & 1, c4 = (tid & 15) * 4;
+      float gv[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float v = ((red[0][r][c4 + q][co] + red[1][r][c4 + q][co]) + red[2][r][c4 + q][co]) + red[3][r][c4 + q][co];
+        gv[q] = (v + bias[co]) / sg;
+      }
+      const float4 g4 = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      const size_t e = (((size_t)b * 2 + co) * H + y0 + r) * W + x0 + c4;
+      if (out) *reinterpret_cast<float4*>(out + e) = g4;
+      float4 l;
+      const float4 o = langevin_group(lg, e / 4, g4, l);
+      reinterpret_cast<float4*>(lg.x)[e / 4] = o;
+      if (lg.lik) reinterpret_cast<float4*>(lg.lik)[e / 4] = l;
+      if (co == 0) lmax = absmax4(o);
+    }
+    if (lg.absmax) block_absmax<4>(lmax, lg.absmax);
   }
 }
 
@@ -486,10 +513,15 @@ hipError_t begin_conv(const float* x, const float* w, const float* bias, float* 
 }
 
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
-                    const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st) {
+                    const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st,
+                    const LangevinArgs* lg) {
   if (Cin != EC_CIN || H % 4 || W % 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(end_conv_kernel, dim3(B * (H / 4) * (W / 64)), dim3(256), 0, st, in, ss, w, bias, sigmas, labels,
-                     out, H, W);
+  const dim3 grid(B * (H / 4) * (W / 64));
+  if (lg)
+    hipLaunchKernelGGL(end_conv_kernel<true>, grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W, *lg);
+  else
+    hipLaunchKernelGGL(end_conv_kernel<false>, grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W,
+                       LangevinArgs{});
   return hipGetLastError();
 }
 

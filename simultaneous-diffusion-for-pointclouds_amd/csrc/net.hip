@@ -207,7 +207,7 @@ struct Fwd {
 
 // ------------------------------------------------------------------------------ forward
 static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, float* out, int B, void* ws,
-                         size_t ws_bytes, hipStream_t st) {
+                         size_t ws_bytes, hipStream_t st, const LangevinArgs* lg = nullptr) {
   const int H = net->d.H, W = net->d.W, C = net->d.ngf, C2 = 2 * C;
   const int h = H / 2, w = W / 2;
   const size_t F = (size_t)B * H * W * C, Q = (size_t)B * h * w * C2;
@@ -293,10 +293,14 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
   Buf o = f.rcu("refine4.output_convs", x2, 3, FA, FB, FD, false, true);           // FB, stats
   // head: IN++ -> ELU -> end_conv -> / sigmas[y]
   f.norm("normalizer", Fwd::tiles(o), 128.f, C);
-  f.prof_launch("end_conv 128->2 @" + std::to_string(H) + "x" + std::to_string(W), (double)B * H * W * (C * 4 + 2 * 4),
-                [&] {
+  // with lg: + the fused Langevin update (x read + written, ref, mask, lik: 20 B per element; the
+  // scores only when out is given)
+  const double lg_bytes = lg ? (double)B * 2 * H * W * (20 + (out ? 4 : 0) + (lg->noise ? 4 : 0)) : B * 2.0 * H * W * 4;
+  f.prof_launch(std::string(lg ? "end_conv+langevin" : "end_conv") + " 128->2 @" + std::to_string(H) + "x" +
+                    std::to_string(W),
+                (double)B * H * W * C * 4 + lg_bytes, [&] {
                   chk(end_conv(o.p, f.ss, net->P("end_conv.weight"), net->P("end_conv.bias"), net->P("sigmas"), labels,
-                               out, B, H, W, C, st),
+                               out, B, H, W, C, st, lg),
                       "end_conv");
                 });
 }
@@ -522,6 +526,22 @@ int sdp_net_forward(sdp_net* net, const float* x, const int64_t* labels, float* 
     chk(hipGraphLaunch(g->exec, st), "hipGraphLaunch");
   } catch (const std::exception& e) {
     return fail(std::string("sdp_net_forward: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_forward_langevin(sdp_net* net, float* x, const int64_t* labels, int B, const sdp_langevin_params* lp,
+                             void* ws, size_t ws_bytes, void* stream) {
+  if (!net || !x || !labels || !lp || !lp->ref || !lp->mask || !ws || B <= 0)
+    return fail("sdp_net_forward_langevin: bad argument");
+  if (!net->finalized) return fail("sdp_net_forward_langevin: call sdp_net_finalize first");
+  if (ws_bytes < workspace_bytes(net, B)) return fail("sdp_net_forward_langevin: workspace too small");
+  const LangevinArgs lg{x,         lp->ref,          lp->mask,  lp->noise,    lp->seed,         lp->offset, lp->step_size,
+                        lp->noise_scale, lp->grad_ref, lp->nan_to_num, lp->lik_out, lp->absmax_bits};
+  try {
+    forward_impl(net, x, labels, lp->grad_out, B, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream), &lg);
+  } catch (const std::exception& e) {
+    return fail(std::string("sdp_net_forward_langevin: ") + e.what());
   }
   return 0;
 }

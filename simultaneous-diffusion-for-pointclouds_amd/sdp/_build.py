@@ -37,6 +37,20 @@ def source_hash() -> str:
     return h.hexdigest()
 
 
+CONV_SOURCES = ("common.h", "conv_kernel.h", "conv.hip")
+
+
+def conv_source_hash() -> str:
+    """Hash of the files the forward conv kernel is built from (tools/conv_bench compiles exactly
+    these): the key of the PMC traffic record bench.py reports (profiles/*_traffic.json)."""
+    h = hashlib.sha256()
+    for f in CONV_SOURCES:
+        h.update(f.encode())
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def _stamp_ok(digest: str) -> bool:
     if not os.path.exists(LIB_PATH) or not os.path.exists(STAMP):
         return False

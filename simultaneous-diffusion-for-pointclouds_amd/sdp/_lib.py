@@ -30,6 +30,12 @@ class MergeParams(C.Structure):
     _fields_ = [("variant", I), ("setting", I), ("sigma", F), ("allowance", F), ("cc", F)]
 
 
+class LangevinParams(C.Structure):
+    _fields_ = [("ref", P), ("mask", P), ("noise", P), ("seed", U64), ("offset", U64), ("step_size", F),
+                ("noise_scale", F), ("grad_ref", F), ("nan_to_num", I), ("lik_out", P), ("absmax_bits", P),
+                ("grad_out", P)]
+
+
 PREC = {"fp32": 0, "fp32x3": 1, "bf16": 2}
 MERGE_POSES, MERGE_ORIGINS = 0, 1
 
@@ -41,6 +47,7 @@ _SIGS = {
     "sdp_net_finalize": (I, [P]),
     "sdp_net_workspace_size": (I, [P, I, C.POINTER(SZ)]),
     "sdp_net_forward": (I, [P, P, P, P, I, P, SZ, P]),
+    "sdp_net_forward_langevin": (I, [P, P, P, I, C.POINTER(LangevinParams), P, SZ, P]),
     "sdp_net_destroy": (I, [P]),
     "sdp_net_profile_enable": (I, [P, I]),
     "sdp_net_profile_read": (I, [P, C.c_char_p, SZ, C.POINTER(I)]),

@@ -6,7 +6,8 @@
 
 Each step is: ``scorenet(x, labels)`` (libsdp forward, or any callable returning a device
 tensor), the fused Langevin kernel (update + max|x[:,0]| for tooHigh), and -- from level
-``minStepToShare`` on -- the device consistency merge.  Host-side scalars (step size, noise
+``minStepToShare`` on -- the device consistency merge.  With libsdp's ScoreNet the first two are
+one call (``forward_langevin``: the update runs in the net's last kernel, bit-identical).  Host-side scalars (step size, noise
 scale, correlation ramps) are computed with the reference's numpy float32 arithmetic.
 
 Keyword-only extras (not in the reference): ``noise_fn(shape) -> tensor`` injects the
@@ -88,16 +89,37 @@ class _Stepper:
             self._labels[c] = t
         return t
 
+    def _noise(self):
+        if self.noise_fn is None:
+            return None
+        return self.noise_fn(tuple(self.x.shape)).to(self.dev, torch.float32).contiguous()
+
     def step(self, grad, step_size, grad_ref, nan_to_num):
         grad = grad.to(self.dev, torch.float32).contiguous()
-        noise = None
-        if self.noise_fn is not None:
-            noise = self.noise_fn(tuple(self.x.shape)).to(self.dev, torch.float32).contiguous()
+        noise = self._noise()
         nscale = F32(np.sqrt(F32(step_size * F32(2))))
         self.absmax.zero_()
         self.ops.langevin(self.x, grad, self.ref, self.mask, noise, self.seed, self.offset, step_size, nscale,
                           grad_ref, nan_to_num, self.lik, self.absmax)
         self.offset += self.offset_stride
+
+    def langevin_step(self, scorenet, c, step_size, grad_ref, nan_to_num, want_grad):
+        """scorenet + Langevin update.  On libsdp (DeviceOps and a ScoreNet) the update runs in the
+        net's last kernel (sdp_net_forward_langevin, bit-identical to the two-call form); the
+        scores are materialised only when asked (want_grad: the report of a level).  Returns them
+        (or None)."""
+        if isinstance(self.ops, DeviceOps) and hasattr(scorenet, "forward_langevin"):
+            noise = self._noise()
+            nscale = F32(np.sqrt(F32(step_size * F32(2))))
+            grad = torch.empty_like(self.x) if want_grad else None
+            self.absmax.zero_()
+            scorenet.forward_langevin(self.x, self.labels(c), self.ref, self.mask, noise, self.seed, self.offset,
+                                      step_size, nscale, grad_ref, nan_to_num, self.lik, self.absmax, grad)
+            self.offset += self.offset_stride
+            return grad
+        grad = scorenet(self.x, self.labels(c))
+        self.step(grad, step_size, grad_ref, nan_to_num)
+        return grad
 
     def denoise(self, grad, sigma_last, grad_ref):
         grad = grad.to(self.dev, torch.float32).contiguous()
@@ -132,13 +154,12 @@ def anneal_Langevin_dynamics_inpainting(x_mod, refer_image, refer_mask, scorenet
     last = None
     for c, sigma in enumerate(sigmas):
         step = _step_size(step_lr, sigma, sigmas[-1])
-        for _ in range(n_steps_each):
-            grad = scorenet(S.x, S.labels(c))
-            S.step(grad, step, grad_ref, nan_to_num=False)
+        for i in range(n_steps_each):
+            grad = S.langevin_step(scorenet, c, step, grad_ref, False, verbose and c % 20 == 0 and i == n_steps_each - 1)
             if keep_all:
                 images.append(S.x.to("cpu"))
             last = grad
-        if verbose and c % 20 == 0:
+        if verbose and c % 20 == 0 and last is not None:
             S.report(grad_ref, c, step, last)
     if not keep_all and len(sigmas) * n_steps_each > 0:
         images.append(S.x.to("cpu"))
@@ -172,9 +193,9 @@ def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr,
         cc = cc_ramp(cc, c, L)
         step = _step_size(step_lr, sigma, sigmas[-1])
         grad = None
-        for _ in range(n_steps_each):
-            grad = scorenet(S.x, S.labels(c))
-            S.step(grad, step, grad_ref, nan_to_num=True)
+        report = print_rule(c, verbose)
+        for i in range(n_steps_each):
+            grad = S.langevin_step(scorenet, c, step, grad_ref, True, report and i == n_steps_each - 1)
             if c >= min_step:
                 if view_split:
                     _gather_views(S, dist_group)

@@ -92,6 +92,34 @@ class ScoreNet:
 
     __call__ = forward
 
+    def forward_langevin(self, x: torch.Tensor, y: torch.Tensor, ref: torch.Tensor, mask: torch.Tensor,
+                         noise: torch.Tensor | None, seed: int, offset: int, step: float, nscale: float,
+                         grad_ref: float, nan_to_num: bool, lik: torch.Tensor | None, absmax: torch.Tensor | None,
+                         grad_out: torch.Tensor | None = None) -> None:
+        """One Langevin step with the update fused into the net's last kernel
+        (sdp_net_forward_langevin): x is updated in place exactly as ``forward`` followed by
+        sdp_langevin_step would; grad_out (optional) receives the scores."""
+        if not self._ready:
+            raise RuntimeError("ScoreNet: load weights first")
+        if not x.is_cuda or x.dtype != torch.float32 or x.dim() != 4 or x.shape[1:] != (self.channels, self.H, self.W) \
+                or not x.is_contiguous():
+            raise ValueError(f"forward_langevin expects contiguous cuda float32 [B,{self.channels},{self.H},{self.W}] "
+                             f"(updated in place), got {tuple(x.shape)} {x.dtype} {x.device}")
+        for name, t, dt in (("ref", ref, torch.float32), ("mask", mask, torch.int32), ("noise", noise, torch.float32),
+                            ("lik", lik, torch.float32), ("grad_out", grad_out, torch.float32)):
+            if t is not None and (t.shape != x.shape or t.dtype != dt or not t.is_contiguous() or t.device != x.device):
+                raise ValueError(f"forward_langevin: {name} must be contiguous {dt} {tuple(x.shape)} on {x.device}")
+        if absmax is not None and (absmax.dtype != torch.int32 or absmax.device != x.device):
+            raise ValueError("forward_langevin: absmax must be an int32 device tensor")
+        B = x.shape[0]
+        y = y.to(device=x.device, dtype=torch.int64).contiguous()
+        ws = self.workspace(B, x.device)
+        p = _lib.LangevinParams(ref.data_ptr(), mask.data_ptr(), _lib.ptr(noise), int(seed) & 0xFFFFFFFFFFFFFFFF,
+                                int(offset), float(step), float(nscale), float(grad_ref), 1 if nan_to_num else 0,
+                                _lib.ptr(lik), _lib.ptr(absmax), _lib.ptr(grad_out))
+        _lib.check(_lib.lib().sdp_net_forward_langevin(self._h, x.data_ptr(), y.data_ptr(), B, _lib.C.byref(p),
+                                                       ws.data_ptr(), ws.numel(), _lib.stream()), "net_forward_langevin")
+
     # ------------------------------------------------------------------ measurement
     def profile(self, enable: bool = True):
         _lib.check(_lib.lib().sdp_net_profile_enable(self._h, 1 if enable else 0), "profile_enable")

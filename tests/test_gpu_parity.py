@@ -3,7 +3,8 @@
 Tolerances (stated once, used below):
   * score net, fp32x3 (3-pass bf16 split MFMA): max|err| <= 1e-4 * max|ref| per image
   * score net, fp32 (exact fp32 MFMA):           max|err| <= 2e-5 * max|ref| per image
-  * Langevin update: bit-exact (same float32 ops and order, injected noise)
+  * Langevin update: bit-exact (same float32 ops and order, injected noise); the update fused
+    into the score net's last kernel: bit-identical to the two-call form
   * merge: new images / corrected x within rtol 1e-5, atol 2e-6 on all but <= 1e-4 of the
     pixels (float64 atan2/log2 of the GPU vs glibc can move a point sitting exactly on a
     bin edge); the known/unknown mask pattern must agree on the same fraction.
@@ -130,6 +131,65 @@ def test_philox_view_shard_draws_the_single_process_stream():
     full = run(4, 3 * 4 * per_view4)            # step 3 of the single-process run
     part = run(2, 3 * 4 * per_view4 + 2 * per_view4)
     np.testing.assert_array_equal(part, full[2:])
+
+
+@pytest.mark.parametrize("noise_kind", ["philox", "injected"])
+def test_fused_forward_langevin_bit_identical(net256, noise_kind):
+    """sdp_net_forward_langevin (update in the end_conv epilogue) == sdp_net_forward followed by
+    sdp_langevin_step, bit for bit: x, lik, max|x[:,0]| and the scores; Philox at a nonzero
+    counter, or an injected noise buffer."""
+    from sdp import _lib
+    B, H, W = 2, 64, 256
+    case = GI.merge_case("langevin", B, H, W)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    x0, ref, mask = t(case["x"]), t(case["ref"]), t(case["mask"])
+    y = torch.tensor([3, 150], device=DEV)
+    noise = t(GI.noise("fused", 0, (B, 2, H, W))) if noise_kind == "injected" else None
+    sig = __import__("sdp").get_sigmas_np()
+    s = S.step_size_of(6.2e-6, sig[150], sig[-1])
+    ns = np.float32(np.sqrt(np.float32(s * np.float32(2))))
+    seed, offset = 4321, 7 * B * 2 * H * W // 4
+
+    x_a = x0.clone()
+    g_a = net256(x_a, y)
+    lik_a = torch.empty_like(x_a)
+    am_a = torch.zeros(1, dtype=torch.int32, device=DEV)
+    _lib.check(_lib.lib().sdp_langevin_step(x_a.data_ptr(), g_a.data_ptr(), ref.data_ptr(), mask.data_ptr(),
+                                            _lib.ptr(noise), seed, offset, float(s), float(ns), 0.7, 1, B, 2, H * W,
+                                            lik_a.data_ptr(), am_a.data_ptr(), _lib.stream()))
+    x_b = x0.clone()
+    lik_b = torch.empty_like(x_b)
+    am_b = torch.zeros(1, dtype=torch.int32, device=DEV)
+    g_b = torch.empty_like(x_b)
+    net256.forward_langevin(x_b, y, ref, mask, noise, seed, offset, float(s), float(ns), 0.7, True, lik_b, am_b, g_b)
+    torch.testing.assert_close(g_b, g_a, rtol=0, atol=0)
+    torch.testing.assert_close(x_b, x_a, rtol=0, atol=0)
+    torch.testing.assert_close(lik_b, lik_a, rtol=0, atol=0)
+    assert am_b.item() == am_a.item() != 0
+    # without the optional outputs the update is the same
+    x_c = x0.clone()
+    net256.forward_langevin(x_c, y, ref, mask, noise, seed, offset, float(s), float(ns), 0.7, True, None, None)
+    torch.testing.assert_close(x_c, x_a, rtol=0, atol=0)
+
+
+def test_sampler_fused_path_equals_two_call_path(net256):
+    """The samplers take the fused path with libsdp's ScoreNet; hiding forward_langevin (a plain
+    callable) gives the two-call path: same images, bit for bit (Philox noise, verbose reports)."""
+    from sdp.sampling import anneal_Langevin_dynamics_inpainting
+    case = GI.merge_case("langevin", 2, 64, 256)
+    sig = __import__("sdp").get_sigmas_np()[[0, 40, 231]]
+
+    def run(scorenet):
+        x = torch.from_numpy(case["x"]).to(DEV)
+        imgs, _ = anneal_Langevin_dynamics_inpainting(x, torch.from_numpy(case["ref"]), torch.from_numpy(case["mask"]),
+                                                      scorenet, sig, n_steps_each=2, verbose=True, seed=99)
+        return [i.numpy() for i in imgs]
+
+    fused = run(net256)
+    plain = run(lambda x, y: net256(x, y))
+    assert len(fused) == len(plain)
+    for a, b in zip(fused, plain):
+        np.testing.assert_array_equal(a, b)
 
 
 def _after_update(case):

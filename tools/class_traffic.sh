@@ -1,8 +1,9 @@
 #!/bin/bash
 # HBM traffic per launch of the dominant conv class (conv3x3 256->256 @32x512 d1, 4 views), measured
 # by PMC on isolated launches of the library's own kernel (tools/conv_bench, built from csrc/conv.hip)
-# for fp32x3 and fp32, written as profiles/<ROUND>_traffic.json tagged with the csrc source hash that
-# bench.py checks before printing roofline.traffic.  Passes: one --pmc group per run, --kernel-trace only.
+# for fp32x3 and fp32, written as profiles/<ROUND>_traffic.json tagged with the hash of the conv sources
+# the binary was built from (tools/_cb/conv_bench_0.hash), which bench.py checks before printing
+# roofline.traffic.  Passes: one --pmc group per run, --kernel-trace only.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -32,7 +33,10 @@ for mode, prec in ((1, "fp32x3"), (0, "fp32")):
                  "algorithmic_bytes": 2 * 4 * 32 * 512 * 256 * 4 + 256 * 256 * 9 * 4,
                  "how": "rocprofv3 --pmc TCC_EA0_RDREQ/WRREQ on isolated launches (tools/conv_bench, affine+ELU "
                         "prologue, circular, 4 views)"})
-doc = {"source_hash": _build.source_hash(), "rows": rows}
+built = open("tools/_cb/conv_bench_0.hash").read().split()
+if built[0] != _build.conv_source_hash() or len(built) > 1:
+    sys.exit(f"tools/_cb/conv_bench_0 was built from other conv sources/flags ({built}): rebuild it (KOS=0 tools/conv_bench.sh)")
+doc = {"conv_source_hash": built[0], "rows": rows}
 dst = f"{out}/{rnd}_traffic.json"   # merged back under gpurun_out/; copied into profiles/ by hand
 json.dump(doc, open(dst, "w"), indent=1)
 print(json.dumps(doc, indent=1))
