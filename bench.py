@@ -76,6 +76,8 @@ def parse():
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 prints the world it saw")
     ap.add_argument("--no-fp32-line", action="store_true",
                     help="skip the exact-fp32 (v_mfma_f32_32x32x2_f32) companion measurement of the line workload")
+    ap.add_argument("--split", type=int, default=0,
+                    help="part-batch streams per score-net forward (sdp_net_set_split; 0 = library default)")
     ap.add_argument("--unfused", action="store_true",
                     help="line/allforone: score net and Langevin update as two calls (sdp_net_forward + "
                          "sdp_langevin_step) instead of sdp_net_forward_langevin")
@@ -258,6 +260,8 @@ def run_sampling(args, rank, N, dist, dev):
         separate profiled pass of a few steps for the per-kernel rooflines; return (dt, roofline)."""
         net_box[0] = net if prec == args.precision else ScoreNet(H=H, W=W, precision=prec).load_synthetic()
         cur = net_box[0]
+        if args.split:
+            cur.set_split(args.split)
         cur.profile(False)
         for i in range(warmup):
             step(i)

@@ -90,6 +90,11 @@ typedef struct {
 } sdp_langevin_params;
 int sdp_net_forward_langevin(sdp_net* net, float* x, const int64_t* labels, int B, const sdp_langevin_params* params,
                              void* workspace, size_t workspace_bytes, void* stream);
+/* Performance knob: run sdp_net_forward / sdp_net_forward_langevin as `ways` part-batch forwards on
+ * that many streams (the caller's + the handle's own, joined before return; 1 = one launch per
+ * layer, 0 = the default: env SDP_SPLIT, else 2).  Results are identical for every value; the
+ * workspace size depends on it (query sdp_net_workspace_size after setting it).              */
+int sdp_net_set_split(sdp_net* net, int ways);
 /* Measurement hooks: when enabled, every conv launch of sdp_net_forward is bracketed by HIP
  * events on the forward's stream; sdp_net_profile_read synchronises on them and writes one
  * line per conv class: "class\tlaunches\ttotal_ms\tflops_per_launch\n". */

@@ -5,6 +5,7 @@
 // InstanceNorm++ is split into per-tile statistics written by the producing conv's
 // epilogue + a tiny finalize kernel + an affine/ELU prologue in the consuming conv, so no
 // activation is ever re-read just for normalisation.
+#include <algorithm>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -305,11 +306,92 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
                 });
 }
 
-static size_t workspace_bytes(const sdp_net* net, int B) {
+static size_t workspace_bytes_one(const sdp_net* net, int B) {
   const int H = net->d.H, W = net->d.W, C = net->d.ngf, C2 = 2 * C;
   const size_t F = (size_t)B * H * W * C, Q = (size_t)B * (H / 2) * (W / 2) * C2;
   auto r = [](size_t n) { return ((n * 4 + 255) / 256) * 256; };
   return r((size_t)B * (H * W / 64) * C2 * 2) + r((size_t)B * C2 * 2) + r((size_t)B * C2 * 4) + 6 * r(F) + 8 * r(Q);
+}
+
+// default of sdp_net::split: SDP_SPLIT=k runs the forward as k part-batch forwards on k streams
+// (forward_split); 1 = off
+static int split_default() {
+  static const int k = [] {
+    const char* e = getenv("SDP_SPLIT");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > SDP_MAX_SPLIT ? SDP_MAX_SPLIT : v);
+  }();
+  return k;
+}
+static int split_ways(const sdp_net* net) { return net->split > 0 ? net->split : split_default(); }
+
+// part p of B images split k ways: [first, first + count)
+static void split_part(int B, int k, int p, int& first, int& count) {
+  first = (int)((long)B * p / k);
+  count = (int)((long)B * (p + 1) / k) - first;
+}
+
+// room for one B-image forward, or for the part-batch forwards side by side (forward_split)
+static size_t workspace_bytes(const sdp_net* net, int B) {
+  size_t need = workspace_bytes_one(net, B);
+  const int k = std::min(B, split_ways(net));
+  if (k > 1) {
+    size_t sum = 0;
+    for (int p = 0; p < k; ++p) {
+      int f, c;
+      split_part(B, k, p, f, c);
+      sum += workspace_bytes_one(net, c);
+    }
+    need = std::max(need, sum);
+  }
+  return need;
+}
+
+// The forward as k part-batch forwards on k streams (the caller's and the handle's own), joined by
+// events.  Every conv launch of one forward is a lock-step grid: each workgroup owns a CU (LDS),
+// so all of them stage their first chunks together and store their outputs together, and those
+// bursts leave the matrix cores idle chip-wide; a grid that is not a whole number of rounds also
+// idles CUs in its last one.  Concurrent part-size launches de-phase the bursts of one against the
+// main loops of another and fill each other's last rounds.  Per-image results are unchanged: no op
+// couples images (batch invariance), and the Langevin update of a part uses its own Philox counters
+// (offset + first image * per-image counters).
+static void forward_split(sdp_net* net, const float* x, const int64_t* labels, float* out, int B, void* ws,
+                          size_t ws_bytes, hipStream_t st, const LangevinArgs* lg) {
+  const int k = std::min(B, split_ways(net));
+  if (k < 2 || net->profile) {
+    forward_impl(net, x, labels, out, B, ws, ws_bytes, st, lg);
+    return;
+  }
+  for (int p = 0; p + 1 < k; ++p) {
+    if (!net->aux_stream[p])
+      chk(hipStreamCreateWithFlags(&net->aux_stream[p], hipStreamNonBlocking), "hipStreamCreate");
+    if (!net->ev_join[p]) chk(hipEventCreateWithFlags(&net->ev_join[p], hipEventDisableTiming), "hipEventCreate");
+  }
+  if (!net->ev_fork) chk(hipEventCreateWithFlags(&net->ev_fork, hipEventDisableTiming), "hipEventCreate");
+  const size_t per = (size_t)2 * net->d.H * net->d.W;        // floats of one image (2 channels)
+  char* w = reinterpret_cast<char*>(ws);
+  chk(hipEventRecord(net->ev_fork, st), "hipEventRecord");
+  for (int p = k - 1; p >= 0; --p) {                        // the caller's stream takes part 0, last
+    int f, c;
+    split_part(B, k, p, f, c);
+    const size_t wb = workspace_bytes_one(net, c);
+    hipStream_t s = p ? net->aux_stream[p - 1] : st;
+    if (p) chk(hipStreamWaitEvent(s, net->ev_fork, 0), "hipStreamWaitEvent");
+    LangevinArgs l{};
+    if (lg) {
+      l = *lg;
+      l.x = lg->x + f * per;
+      l.ref = lg->ref + f * per;
+      l.mask = lg->mask + f * per;
+      if (lg->noise) l.noise = lg->noise + f * per;
+      if (lg->lik) l.lik = lg->lik + f * per;
+      l.offset = lg->offset + f * per / 4;
+    }
+    forward_impl(net, x + f * per, labels + f, out ? out + f * per : nullptr, c, w, wb, s, lg ? &l : nullptr);
+    w += wb;
+    if (p) chk(hipEventRecord(net->ev_join[p - 1], s), "hipEventRecord");
+  }
+  for (int p = 0; p + 1 < k; ++p) chk(hipStreamWaitEvent(st, net->ev_join[p], 0), "hipStreamWaitEvent");
 }
 
 // SDP_GRAPH=1 turns on the forward's HIP-graph replay (never while profiling).  Off by default:
@@ -477,7 +559,7 @@ int sdp_net_forward(sdp_net* net, const float* x, const int64_t* labels, float* 
   const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   try {
     if (net->profile || !graphs_enabled()) {
-      forward_impl(net, x, labels, out, B, ws, ws_bytes, st);
+      forward_split(net, x, labels, out, B, ws, ws_bytes, st, nullptr);
       return 0;
     }
     // HIP-graph replay: ~130 launches per forward cost one graph launch; the captured kernels
@@ -539,10 +621,16 @@ int sdp_net_forward_langevin(sdp_net* net, float* x, const int64_t* labels, int 
   const LangevinArgs lg{x,         lp->ref,          lp->mask,  lp->noise,    lp->seed,         lp->offset, lp->step_size,
                         lp->noise_scale, lp->grad_ref, lp->nan_to_num, lp->lik_out, lp->absmax_bits};
   try {
-    forward_impl(net, x, labels, lp->grad_out, B, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream), &lg);
+    forward_split(net, x, labels, lp->grad_out, B, ws, ws_bytes, reinterpret_cast<hipStream_t>(stream), &lg);
   } catch (const std::exception& e) {
     return fail(std::string("sdp_net_forward_langevin: ") + e.what());
   }
+  return 0;
+}
+
+int sdp_net_set_split(sdp_net* net, int ways) {
+  if (!net || ways < 0 || ways > SDP_MAX_SPLIT) return fail("sdp_net_set_split: ways must be 0 (default) .. 4");
+  net->split = ways;
   return 0;
 }
 

@@ -27,6 +27,8 @@ inline void chk(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
+constexpr int SDP_MAX_SPLIT = 4;   // part-batch streams of one forward (net.hip forward_split)
+
 struct TrainPlan;   // train.hip
 void destroy_plan(TrainPlan* p);
 
@@ -69,6 +71,9 @@ struct sdp_net {
   std::vector<GraphEntry> graphs;
   unsigned long long graph_clock = 0;
   hipStream_t cap_stream = nullptr;
+  int split = 0;                     // part-batch forwards (0: SDP_SPLIT, default 2)
+  hipStream_t aux_stream[sdp::SDP_MAX_SPLIT - 1] = {};   // part-batch forwards 1.. (net.hip forward_split)
+  hipEvent_t ev_fork = nullptr, ev_join[sdp::SDP_MAX_SPLIT - 1] = {};
   int64_t* lab_dev = nullptr;       // [lab_cap] labels of the replayed forwards
   int lab_cap = 0;
   void drop_graphs() {
@@ -79,6 +84,11 @@ struct sdp_net {
   ~sdp_net() {
     release();
     if (cap_stream) (void)hipStreamDestroy(cap_stream);
+    for (auto& s : aux_stream)
+      if (s) (void)hipStreamDestroy(s);
+    for (auto& e : ev_join)
+      if (e) (void)hipEventDestroy(e);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (lab_dev) (void)hipFree(lab_dev);
     for (auto& r : prof) {
       (void)hipEventDestroy(r.a);

@@ -120,6 +120,12 @@ class ScoreNet:
         _lib.check(_lib.lib().sdp_net_forward_langevin(self._h, x.data_ptr(), y.data_ptr(), B, _lib.C.byref(p),
                                                        ws.data_ptr(), ws.numel(), _lib.stream()), "net_forward_langevin")
 
+    def set_split(self, ways: int):
+        """Run each forward as `ways` part-batch forwards on as many streams (0 = default: env
+        SDP_SPLIT, else 2; 1 = off).  Results are identical; only the launch schedule changes."""
+        _lib.check(_lib.lib().sdp_net_set_split(self._h, int(ways)), "set_split")
+        self._ws.clear()                    # the workspace size depends on it
+
     # ------------------------------------------------------------------ measurement
     def profile(self, enable: bool = True):
         _lib.check(_lib.lib().sdp_net_profile_enable(self._h, 1 if enable else 0), "profile_enable")

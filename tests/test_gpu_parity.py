@@ -172,6 +172,36 @@ def test_fused_forward_langevin_bit_identical(net256, noise_kind):
     torch.testing.assert_close(x_c, x_a, rtol=0, atol=0)
 
 
+def test_split_forward_is_bit_identical(net256):
+    """sdp_net_set_split: 1, 2, 3 and 4 part-batch streams give the same scores and the same fused
+    Langevin update, bit for bit (B=5: uneven parts)."""
+    from sdp import _lib
+    B, H, W = 5, 64, 256
+    case = GI.merge_case("split", B, H, W)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    x0, ref, mask = t(case["x"]), t(case["ref"]), t(case["mask"])
+    y = torch.tensor([0, 17, 99, 150, 231], device=DEV)
+    outs = []
+    try:
+        for ways in (1, 2, 3, 4):
+            net256.set_split(ways)
+            g = net256(x0, y)
+            x = x0.clone()
+            lik = torch.empty_like(x)
+            am = torch.zeros(1, dtype=torch.int32, device=DEV)
+            net256.forward_langevin(x, y, ref, mask, None, 5, 1234, 1e-5, 4e-3, 0.5, True, lik, am)
+            outs.append((g.cpu(), x.cpu(), lik.cpu(), am.item()))
+    finally:
+        net256.set_split(0)
+    for g, x, lik, am in outs[1:]:
+        torch.testing.assert_close(g, outs[0][0], rtol=0, atol=0)
+        torch.testing.assert_close(x, outs[0][1], rtol=0, atol=0)
+        torch.testing.assert_close(lik, outs[0][2], rtol=0, atol=0)
+        assert am == outs[0][3]
+    with pytest.raises(RuntimeError):
+        _lib.check(_lib.lib().sdp_net_set_split(net256._h, 5), "set_split")
+
+
 def test_sampler_fused_path_equals_two_call_path(net256):
     """The samplers take the fused path with libsdp's ScoreNet; hiding forward_langevin (a plain
     callable) gives the two-call path: same images, bit for bit (Philox noise, verbose reports)."""
