@@ -39,6 +39,9 @@ SDP_DEV float wave_sum(float v) {
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int BC_TP = 128, BC_RS = 132;            // pixels per tile; staged patch row stride (floats)
+#ifndef SDP_BC_KO   // diagnostic knock-outs (tools/lib_variant.sh only): 1 = no output stores, 2 = no FMAs
+#define SDP_BC_KO 0
+#endif
 constexpr int BC_WG_PER_CU = 3;
 __global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                          const float* __restrict__ bias, float* __restrict__ out,
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const flo
       acc[i][1] = b23;
     }
 #pragma unroll
-    for (int cr = 0; cr < 12; ++cr) {              // (input channel, kernel row)
+    for (int cr = 0; cr < ((SDP_BC_KO & 2) ? 0 : 12); ++cr) {   // (input channel, kernel row)
       float v[18];
       const float* row = sp + cr * BC_RS + 16 * pg;
 #pragma unroll
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const flo
     }
     float* o = out + (((size_t)b * H + y) * W + x0 + 16 * pg) * CO + 4 * cg;
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < ((SDP_BC_KO & 1) ? 0 : 16); ++i)
       __builtin_nontemporal_store(f32x4v{acc[i][0].x, acc[i][0].y, acc[i][1].x, acc[i][1].y},
                                   reinterpret_cast<f32x4v*>(o + (size_t)i * CO));
     // statistics of channel 4cg+j over this thread's 16 pixels, then over 32 (lanes l, l^32 hold
@@ -404,7 +407,10 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
   const int wave = tid >> 6;
   const int C4 = C / 4, CG = C4 / 32;              // 128-channel groups
   const int strips = W / MP_COLS, RB = (H + MP_ROWS - 1) / MP_ROWS;
-  int t = blockIdx.x;
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so give each XCD a contiguous
+  // range -- the strips on either side of a strip (its halo columns) then sit in the same L2
+  const int nwg = gridDim.x;
+  int t = (nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3);
   const int cg = t % CG;
   t /= CG;
   const int strip = t % strips;
