@@ -395,7 +395,7 @@ __global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict
 // max_pool2d keeps for its backward.  For it the edge copies are overwritten with -inf (an edge
 // copy sits earlier in window order than its original and would take the tie), so -inf padding
 // never wins.
-constexpr int MP_ROWS = 16, MP_COLS = 8, MP_NS = 8, MP_D = 4;
+constexpr int MP_ROWS = 16, MP_COLS = 8, MP_NS = 6, MP_D = 2;
 template <bool IDX>
 __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
                                                        uchar4* __restrict__ idx, int B, int H, int W, int C) {
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
     const int slot = (j + 4) % MP_NS;
     if (wave < 2) __builtin_amdgcn_s_waitcnt(0x0f70 | (WAIT01 & 15) | ((WAIT01 >> 4) << 14));
     else __builtin_amdgcn_s_waitcnt(0x0f70 | (WAIT23 & 15) | ((WAIT23 >> 4) << 14));
-    if (j >= 4) pad_row(y + 2, slot);
+    if (j >= MP_D) pad_row(y + 2, slot);           // rows past the prologue were landed in the loop
     __syncthreads();                               // row y+2 landed everywhere; row j+4+MP_D-MP_NS consumed
     hmax(slot, hm[4], hc[4]);
     dma_row(y + 2 + MP_D, (j + 4 + MP_D) % MP_NS);
