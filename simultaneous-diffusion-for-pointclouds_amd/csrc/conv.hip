@@ -1,49 +1,24 @@
-// Launchers of the forward convolutions of NCSN_LiDAR_small (kernel: conv_kernel.h).
+// Shape dispatch of the forward convolutions of NCSN_LiDAR_small (kernel: conv_kernel.h;
+// launchers: conv_launch.h, instantiated per shape in conv_inst.hip).
 #include <cstdlib>
 
-#include "conv_kernel.h"
+#include "conv_launch.h"
 
 namespace sdp {
 
-// ----------------------------------------------------------------------------- launch
-// MFMA shape of the forward bf16-mode launches (conv_kernel.h SH): 16 unless SDP_MFMA_SHAPE=32
-static int mfma_shape() {
-  static const int sh = [] {
-    const char* e = getenv("SDP_MFMA_SHAPE");
-    return (e && atoi(e) == 32) ? 32 : 16;
-  }();
-  return sh;
-}
-
-template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
-static hipError_t launch_t(ConvArgs a, hipStream_t st) {
-  using T = ConvTile<WM, TC, KS>;
-  a.tiles_per_img = a.H * a.W / (T::TR * TC);
-  a.groups_per_img = a.H * a.W / 128;
-  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  if constexpr (MODE != MODE_F32) {
-    if (!a.dact && mfma_shape() == 16) {
-      hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16>), grid, dim3(256), 0, st, a);
-      return hipGetLastError();
-    }
-  }
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
 template <int MODE, bool PELU>
 static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
-  if (ks == 1) return launch_t<MODE, 1, 64, 1, true, PELU>(a, st);   // only the ConvMeanPool 1x1 shortcut
-  if (pool) return launch_t<MODE, 1, 64, 3, true, PELU>(a, st);
-  if (wm == 2) return launch_t<MODE, 2, 32, 3, false, PELU>(a, st);
-  return tc == 64 ? launch_t<MODE, 1, 64, 3, false, PELU>(a, st) : launch_t<MODE, 1, 32, 3, false, PELU>(a, st);
+  if (ks == 1) return conv_launch<MODE, 1, 64, 1, true, PELU>(a, st);   // only the ConvMeanPool 1x1 shortcut
+  if (pool) return conv_launch<MODE, 1, 64, 3, true, PELU>(a, st);
+  if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, PELU>(a, st);
+  return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, PELU>(a, st) : conv_launch<MODE, 1, 32, 3, false, PELU>(a, st);
 }
 
 template <int MODE>
 static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
 #ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
-  if (wm == 2) return launch_t<MODE, 2, 32, 3, false, true>(a, st);
-  return tc == 64 ? launch_t<MODE, 1, 64, 3, false, true>(a, st) : launch_t<MODE, 1, 32, 3, false, true>(a, st);
+  if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, true>(a, st);
+  return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, true>(a, st) : conv_launch<MODE, 1, 32, 3, false, true>(a, st);
 #else
   return a.pro_mode == PRO_NONE ? launch_elu<MODE, false>(a, ks, pool, wm, tc, st)
                                 : launch_elu<MODE, true>(a, ks, pool, wm, tc, st);

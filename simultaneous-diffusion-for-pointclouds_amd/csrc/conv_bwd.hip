@@ -8,39 +8,16 @@
 // (ConvArgs::dact) and the residual add of the gradient already accumulated for its input.
 #include <cstdlib>
 
-#include "conv_kernel.h"
+#include "conv_launch.h"
 
 namespace sdp {
 
-// MFMA shape of the data-gradient launches (conv_kernel.h SH; the LDS-staged epilogue handles
-// both): 16 unless SDP_DGRAD_SHAPE=32
-static int dgrad_shape() {
-  static const int sh = [] {
-    const char* e = getenv("SDP_DGRAD_SHAPE");
-    return (e && atoi(e) == 32) ? 32 : 16;
-  }();
-  return sh;
-}
-
-template <int MODE, int WM, int TC, int KS, bool ZP>
-static hipError_t launch_dgrad_t(ConvArgs a, hipStream_t st) {
-  using T = ConvTile<WM, TC, KS>;
-  a.tiles_per_img = a.H * a.W / (T::TR * TC);
-  a.groups_per_img = a.H * a.W / 128;
-  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  if (dgrad_shape() == 16)
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
 template <int MODE>
 static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, hipStream_t st) {
-  if (ks == 1) return launch_dgrad_t<MODE, 2, 32, 1, false>(a, st);
-  if (!a.circular) return launch_dgrad_t<MODE, 2, 32, 3, true>(a, st);
-  if (wm == 2) return launch_dgrad_t<MODE, 2, 32, 3, false>(a, st);
-  return tc == 64 ? launch_dgrad_t<MODE, 1, 64, 3, false>(a, st) : launch_dgrad_t<MODE, 1, 32, 3, false>(a, st);
+  if (ks == 1) return dgrad_launch<MODE, 2, 32, 1, false>(a, st);
+  if (!a.circular) return dgrad_launch<MODE, 2, 32, 3, true>(a, st);
+  if (wm == 2) return dgrad_launch<MODE, 2, 32, 3, false>(a, st);
+  return tc == 64 ? dgrad_launch<MODE, 1, 64, 3, false>(a, st) : dgrad_launch<MODE, 1, 32, 3, false>(a, st);
 }
 
 // a.in = dy [B][H][W][Cin = forward Cout], a.wf = dgrad-packed weights, a.out = dx

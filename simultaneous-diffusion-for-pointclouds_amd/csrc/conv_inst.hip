@@ -1,0 +1,101 @@
+// Definitions + explicit instantiations of the conv launchers (conv_launch.h).
+//
+// Built once per kernel shape (Makefile: conv_i_<code>.o with -DSDP_INST=<code>):
+//   forward : code = 100 * (mode + 1) + 10 * pelu + shape   (shape = index into FwdShape)
+//   dgrad   : code = 1000 + 10 * mode + shape                (shape = index into DgradShape)
+// Without SDP_INST (tools/conv_bench, -DSDP_CONV_BENCH_ONLY) it instantiates the 3x3 non-pooled
+// ELU-prologue forward shapes of every mode, which is all that bench dispatches.
+#include <cstdlib>
+
+#include "conv_kernel.h"
+#include "conv_launch.h"
+
+namespace sdp {
+
+// MFMA shape of the forward bf16-mode launches (conv_kernel.h SH): 16 unless SDP_MFMA_SHAPE=32
+static int mfma_shape() {
+  static const int sh = [] {
+    const char* e = getenv("SDP_MFMA_SHAPE");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return sh;
+}
+
+// MFMA shape of the data-gradient launches (the LDS-staged epilogue handles both): 16 unless
+// SDP_DGRAD_SHAPE=32
+static int dgrad_shape() {
+  static const int sh = [] {
+    const char* e = getenv("SDP_DGRAD_SHAPE");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return sh;
+}
+
+template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
+hipError_t conv_launch(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<WM, TC, KS>;
+  a.tiles_per_img = a.H * a.W / (T::TR * TC);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  if constexpr (MODE != MODE_F32) {
+    if (!a.dact && mfma_shape() == 16) {
+      hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16>), grid, dim3(256), 0, st, a);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template <int MODE, int WM, int TC, int KS, bool ZP>
+hipError_t dgrad_launch(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<WM, TC, KS>;
+  a.tiles_per_img = a.H * a.W / (T::TR * TC);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  if (dgrad_shape() == 16)
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// the shapes conv.hip / conv_bwd.hip dispatch to
+template <int S> struct FwdShape;
+template <> struct FwdShape<0> { static constexpr int WM = 1, TC = 64, KS = 1; static constexpr bool POOL = true; };
+template <> struct FwdShape<1> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool POOL = true; };
+template <> struct FwdShape<2> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool POOL = false; };
+template <> struct FwdShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool POOL = false; };
+template <> struct FwdShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool POOL = false; };
+template <int S> struct DgradShape;
+template <> struct DgradShape<0> { static constexpr int WM = 2, TC = 32, KS = 1; static constexpr bool ZP = false; };
+template <> struct DgradShape<1> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool ZP = true; };
+template <> struct DgradShape<2> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool ZP = false; };
+template <> struct DgradShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool ZP = false; };
+template <> struct DgradShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool ZP = false; };
+
+#if defined(SDP_INST) && SDP_INST < 1000
+constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
+static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && kShape <= 4, "SDP_INST: bad forward code");
+using FS = FwdShape<kShape>;
+template hipError_t conv_launch<kMode, FS::WM, FS::TC, FS::KS, FS::POOL, (kPelu != 0)>(ConvArgs, hipStream_t);
+#elif defined(SDP_INST)
+constexpr int kMode = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
+static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16) && kShape <= 4,
+              "SDP_INST: bad dgrad code");
+using DS = DgradShape<kShape>;
+template hipError_t dgrad_launch<kMode, DS::WM, DS::TC, DS::KS, DS::ZP>(ConvArgs, hipStream_t);
+#elif defined(SDP_CONV_BENCH_ONLY)
+#define SDP_BENCH_INST(M)                                                           \
+  template hipError_t conv_launch<M, 2, 32, 3, false, true>(ConvArgs, hipStream_t); \
+  template hipError_t conv_launch<M, 1, 64, 3, false, true>(ConvArgs, hipStream_t); \
+  template hipError_t conv_launch<M, 1, 32, 3, false, true>(ConvArgs, hipStream_t);
+SDP_BENCH_INST(MODE_F32)
+SDP_BENCH_INST(MODE_F32X3)
+SDP_BENCH_INST(MODE_BF16)
+#undef SDP_BENCH_INST
+#else
+#error "conv_inst.hip: build with -DSDP_INST=<code> (Makefile) or -DSDP_CONV_BENCH_ONLY (tools/conv_bench)"
+#endif
+
+}  // namespace sdp

@@ -1,0 +1,18 @@
+// Launchers of conv_mfma_kernel, one per kernel shape.  Declared here, defined and explicitly
+// instantiated in conv_inst.hip, which the Makefile compiles once per (mode, prologue, shape) with
+// -DSDP_INST=<code>: every object holds one or two kernels, so `make -j` builds the ~70 kernel
+// instantiations in parallel instead of in two translation units (10 + 4 minutes serial).
+#pragma once
+#include "common.h"
+
+namespace sdp {
+
+// forward conv (conv.hip dispatch): shapes of the table in conv_inst.hip
+template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
+hipError_t conv_launch(ConvArgs a, hipStream_t st);
+
+// data gradient (conv_bwd.hip dispatch)
+template <int MODE, int WM, int TC, int KS, bool ZP>
+hipError_t dgrad_launch(ConvArgs a, hipStream_t st);
+
+}  // namespace sdp

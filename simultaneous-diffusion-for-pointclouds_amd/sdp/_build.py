@@ -37,7 +37,7 @@ def source_hash() -> str:
     return h.hexdigest()
 
 
-CONV_SOURCES = ("common.h", "conv_kernel.h", "conv.hip")
+CONV_SOURCES = ("common.h", "conv_kernel.h", "conv_launch.h", "conv.hip", "conv_inst.hip")
 
 
 def conv_source_hash() -> str:
