@@ -174,6 +174,230 @@ __global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const flo
   }
 }
 
+// ---------------------------------------------------------------- begin conv on MFMA (bf16 modes)
+// The same 128-pixel row tiles, the 4 -> 128 contraction on v_mfma_f32_16x16x32_bf16 with
+// M = 16 output channels, N = 16 pixels, K = (tap, channel) = 36 of 64 (two 32-deep steps;
+// fp32x3 = lo*hi + hi*lo + hi*hi of the bf16 split).  C fragments then hold 4 consecutive channels
+// of one pixel per lane: 16-B stores, a wave pair writes whole 128-B runs.  Wave w owns channels
+// 64 (w & 1) .. +63 and pixels 64 (w >> 1) .. +63 of the tile, i.e. whole 64-pixel statistics
+// groups: (mean, M2) per channel in registers, Chan merges across the 16 pixel lanes.  Persistent;
+// the weight fragments are built once per workgroup, the next tile's image values are loaded into
+// registers (unconditional, clamped loads) while the current tile computes.  The FMA work of the
+// direct kernel (4608 per pixel on packed-f32 VALU) is what kept it off the HBM roofline.
+constexpr int BM_WG_PER_CU = 2, BM_TS = 68;   // workgroups per CU; transpose row stride (floats)
+#ifndef SDP_BC_LDS_T      // 1: output stores through an LDS transpose (256-B runs); 0: straight from the C fragments
+#define SDP_BC_LDS_T 1
+#endif
+#ifndef SDP_BM_KO         // diagnostic knock-outs (tools/lib_variant.sh only): 1 = no output stores, 2 = no
+#define SDP_BM_KO 0       // statistics, 4 = no MFMAs
+#endif
+#ifndef SDP_BC_NT         // 1: nontemporal output stores.  tools/write_bw on MI355X: plain float4 stores of the
+#define SDP_BC_NT 0       // 134 MB output reach 6.1-6.3 TB/s, nt ones 4.9-5.4 (whole rows) / 3.7 (64-B runs)
+#endif
+SDP_DEV void bm_store(f32x4v v, f32x4v* p) {
+  if constexpr (SDP_BC_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+#ifndef SDP_HEAD_DIRECT   // A/B switch (tools/lib_variant.sh only): 1 = the direct fp32 begin/end conv in every mode
+#define SDP_HEAD_DIRECT 0
+#endif
+template <int MODE>
+__global__ __launch_bounds__(256, BM_WG_PER_CU) void begin_conv_mfma_kernel(const float* __restrict__ x,
+                                                                           const float* __restrict__ w,
+                                                                           const float* __restrict__ bias,
+                                                                           float* __restrict__ out,
+                                                                           float* __restrict__ stats, int B, int H, int W) {
+  constexpr int CO = 128, NI = 6 * 130, PE = (NI + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float sp[12 * BC_RS];   // [ci*3 + row][col], cols -1 .. 128
+#if SDP_BC_LDS_T
+  __shared__ __attribute__((aligned(16))) float tbuf[4 * 64 * BM_TS];   // per wave: [64 px][64 ch + pad]
+#endif
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, l16 = lane & 15;
+  const int ch = wave & 1, ph = wave >> 1;
+  const int tiles_row = W / BC_TP, tiles_per_img = H * tiles_row, ntiles = B * tiles_per_img;
+
+  // A (weight) fragments: row co = 64 ch + 16 f + l16, k = 32 s + 8 q + j -> (tap k / 4, ci k % 4)
+  bf16x8 ah[4][2], al[4][2];
+  f32x4 bias4[4];
+#pragma unroll
+  for (int f = 0; f < 4; ++f) {
+    const int co = 64 * ch + 16 * f + l16;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 32 * s + 8 * q + j;
+        const float v = k < 36 ? w[(co * 4 + (k & 3)) * 9 + (k >> 2)] : 0.f;
+        ah[f][s][j] = (__bf16)v;
+        al[f][s][j] = (__bf16)(v - (float)ah[f][s][j]);
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias4[f][r] = bias[64 * ch + 16 * f + 4 * q + r];
+  }
+  // image values of a tile's patch rows (2 channels x 3 rows x 130 columns), clamped addresses
+  float rv[PE];
+  auto load_patch = [&](int t) __attribute__((always_inline)) {
+    t = min(t, ntiles - 1);
+    const int b = t / tiles_per_img, tile = t % tiles_per_img;
+    const int y = tile / tiles_row, x0 = (tile % tiles_row) * BC_TP;
+#pragma unroll
+    for (int k = 0; k < PE; ++k) {
+      const int i = min(tid + k * 256, NI - 1);
+      const int cr = i / 130, c = i % 130, ci = cr / 3, r = cr % 3;
+      const int yy = min(max(y - 1 + r, 0), H - 1), xx = min(max(x0 - 1 + c, 0), W - 1);
+      rv[k] = x[(((size_t)b * 2 + ci) * H + yy) * W + xx];
+    }
+  };
+  load_patch(blockIdx.x);
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int b = t / tiles_per_img, tile = t % tiles_per_img;
+    const int y = tile / tiles_row, x0 = (tile % tiles_row) * BC_TP;
+    __syncthreads();                               // the previous tile's patch is consumed
+#pragma unroll
+    for (int k = 0; k < PE; ++k) {
+      const int i = tid + k * 256;
+      const int cr = i / 130, c = i % 130, r = cr % 3;
+      const int yy = y - 1 + r, xx = x0 - 1 + c;
+      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+      if (i < NI) {
+        sp[cr * BC_RS + c] = ok ? 2.f * rv[k] - 1.f : 0.f;                // channels 0, 1: 2x - 1
+        const float e = cr < 3 ? linspace01(xx, W) : linspace01(yy, H);   // rows 6..11: coordinates
+        sp[(cr + 6) * BC_RS + c] = ok ? e : 0.f;
+      }
+    }
+    __syncthreads();
+    load_patch(t + gridDim.x);                     // the next tile's values fly meanwhile
+    f32x4 acc[4][4];                               // [pixel group g][channel fragment f]
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      // B fragment (im2col): pixel 64 ph + 16 g + l16, k = 32 s + 8 q + j
+      const int px = 64 * ph + 16 * g + l16;
+      float v0[8], v1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 8 * q + j, tap = k >> 2, ci = k & 3;
+        v0[j] = sp[(ci * 3 + tap / 3) * BC_RS + px + tap % 3];
+        const int tap1 = 8;                         // s = 1: only k = 32..35 (tap 8, q = 0, j < 4) are real
+        v1[j] = (q == 0 && j < 4) ? sp[(j * 3 + tap1 / 3) * BC_RS + px + tap1 % 3] : 0.f;
+      }
+      bf16x8 bh0, bl0, bh1, bl1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bh0[j] = (__bf16)v0[j];
+        bl0[j] = (__bf16)(v0[j] - (float)bh0[j]);
+        bh1[j] = (__bf16)v1[j];
+        bl1[j] = (__bf16)(v1[j] - (float)bh1[j]);
+      }
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        f32x4 c = bias4[f];
+        if constexpr (SDP_BM_KO & 4) { acc[g][f] = c + bh0[0] * (float)g; continue; }
+        if constexpr (MODE == MODE_F32X3) {
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[f][0], bh0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f][0], bl0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[f][1], bh1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f][1], bl1, c, 0, 0, 0);
+        }
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f][0], bh0, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[f][1], bh1, c, 0, 0, 0);
+        acc[g][f] = c;
+      }
+    }
+#if SDP_BC_LDS_T
+    // stores through a wave-private LDS transpose: each instruction writes 4 pixels x 256 B (the
+    // wave's 64 channels) instead of 16 pixels x 64 B.  The statistics come from the transposed
+    // values: lane (pq, c4) holds channels 4 c4 .. +3 of pixels 4 i + pq, i < 16 -- a two-pass
+    // (mean, M2) over its 16 pixels, then two equal-count Chan merges (lanes ^16, ^32) -- instead
+    // of 4 levels of cross-lane merges of 16 channels on the C-fragment layout
+    float* tw = tbuf + wave * 64 * BM_TS;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        *reinterpret_cast<f32x4v*>(tw + (16 * g + l16) * BM_TS + 16 * f + 4 * q) =
+            f32x4v{acc[g][f][0], acc[g][f][1], acc[g][f][2], acc[g][f][3]};
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int pq = lane >> 4, c4 = lane & 15;
+    f32x4v tv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tv[i] = *reinterpret_cast<const f32x4v*>(tw + (4 * i + pq) * BM_TS + 4 * c4);
+    if constexpr (!(SDP_BM_KO & 1)) {
+      float* o = out + (((size_t)b * H + y) * W + x0 + 64 * ph + pq) * CO + 64 * ch + 4 * c4;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bm_store(tv[i], reinterpret_cast<f32x4v*>(o + (size_t)4 * i * CO));
+    }
+    if constexpr (SDP_BM_KO & 2) continue;
+    f32x4v mean = tv[0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) mean += tv[i];
+    mean *= (1.f / 16.f);
+    f32x4v m2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const f32x4v dv = tv[i] - mean;
+      m2 += dv * dv;
+    }
+    float2 res[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float mj = mean[j], qj = m2[j], n = 16.f;
+#pragma unroll
+      for (int o2 = 16; o2 < 64; o2 <<= 1) {
+        const float mp = __shfl_xor(mj, o2), qp = __shfl_xor(qj, o2), d = mj - mp;
+        qj = qj + qp + d * d * (0.5f * n);
+        mj = 0.5f * (mj + mp);
+        n *= 2.f;
+      }
+      res[j] = make_float2(mj, qj);
+    }
+    if (pq == 0) {
+      float4* st = reinterpret_cast<float4*>(reinterpret_cast<float2*>(stats) +
+                                             ((size_t)b * (H * W / 64) + (y * W + x0) / 64 + ph) * CO + 64 * ch + 4 * c4);
+      st[0] = make_float4(res[0].x, res[0].y, res[1].x, res[1].y);
+      st[1] = make_float4(res[2].x, res[2].y, res[3].x, res[3].y);
+    }
+  }
+}
+#else
+    if constexpr (!(SDP_BM_KO & 1)) {
+    // stores: lane = 4 channels (64 ch + 16 f + 4 q ..) of pixel x0 + 64 ph + 16 g + l16
+    float* o = out + (((size_t)b * H + y) * W + x0 + 64 * ph + l16) * CO + 64 * ch + 4 * q;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int f = 0; f < 4; ++f)
+        bm_store(f32x4v{acc[g][f][0], acc[g][f][1], acc[g][f][2], acc[g][f][3]},
+                                    reinterpret_cast<f32x4v*>(o + (size_t)16 * g * CO + 16 * f));
+    }
+    if constexpr (SDP_BM_KO & 2) continue;
+    // statistics of this wave's 64-pixel group: 4 values per lane and channel, then the 16 lanes
+    float2* st = reinterpret_cast<float2*>(stats) + ((size_t)b * (H * W / 64) + (y * W + x0) / 64 + ph) * CO + 64 * ch + 4 * q;
+#pragma unroll
+    for (int f = 0; f < 4; ++f)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float mean = 0.25f * (((acc[0][f][r] + acc[1][f][r]) + acc[2][f][r]) + acc[3][f][r]);
+        float m2 = 0.f;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float dv = acc[g][f][r] - mean;
+          m2 = fmaf(dv, dv, m2);
+        }
+        float n = 4.f;
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) {     // equal-count Chan merges
+          const float mp = __shfl_xor(mean, o2), qp = __shfl_xor(m2, o2), d = mean - mp;
+          m2 = m2 + qp + d * d * (0.5f * n);
+          mean = 0.5f * (mean + mp);
+          n *= 2.f;
+        }
+        if (l16 == 0) st[16 * f + r] = make_float2(mean, m2);
+      }
+  }
+}
+#endif
+
 // ---------------------------------------------------------------- end conv (128 -> 2), NCHW out
 // block: 4 rows x 64 cols of output.  The image's IN++ (scale, shift) and the 2 x 128 x 9 weights
 // (as (co0, co1) pairs per (tap, channel)) are staged in LDS once.  Per 32-channel chunk the
@@ -301,6 +525,192 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
       if (co == 0) lmax = absmax4(o);
     }
     if (lg.absmax) block_absmax<4>(lmax, lg.absmax);
+  }
+}
+
+// ---------------------------------------------------------------- end conv on MFMA (bf16 modes)
+// The 128 -> 2 contraction as 18 partials per INPUT pixel, P[q][(tap, co)] = sum_ci e[q][ci] w[co][ci][tap]
+// with e = ELU(IN++(a)), on v_mfma_f32_16x16x32_bf16 (M = 16 input pixels, N = the 18 (tap, co)
+// columns in two 16-wide blocks, K = 32 channels per step; fp32x3 = lo*hi + hi*lo + hi*hi of the
+// bf16 split, as conv_kernel.h), then out[p][co] = bias + sum_tap P[p + d_tap][(tap, co)] from LDS.
+// Block: 16 x 32 output pixels; every pixel of its 18 x 34 input region (1.2x the outputs) is read
+// and transformed ONCE, straight into A fragments (no LDS staging, no per-tap re-transform): the
+// IN++/ELU transform of the direct kernel's 6 x 66 patches (1.55x, once per chunk) was its VALU
+// bound.  Lane l holds pixel l % 16 of a 16-pixel group and the 8 channels {4q..4q+3, 16+4q..16+4q+3}
+// (q = l / 16) of each 32-channel step -- two float4 loads; B uses the same channel order.
+// The (scale, shift) of the lane's 32 channels and the B fragments stay in registers for the block.
+constexpr int E2_TR = 16, E2_TC = 32, E2_PR = E2_TR + 2, E2_PC = E2_TC + 2, E2_NP = E2_PR * E2_PC;
+constexpr int E2_NG = (E2_NP + 15) / 16, E2_PS = 19;   // 16-pixel groups; P row stride (floats)
+#ifndef SDP_EC_DEPTH      // groups in the load ring (2 or 3)
+#define SDP_EC_DEPTH 2
+#endif
+#ifndef SDP_EC_KO         // diagnostic knock-outs (tools/lib_variant.sh only): 1 = no IN++/ELU transform,
+#define SDP_EC_KO 0       // 2 = no MFMAs, 4 = no input loads
+#endif
+#ifndef SDP_EC_SS_LDS     // 1: IN++ (scale, shift) read from LDS per group; 0: held in registers
+#define SDP_EC_SS_LDS 0
+#endif
+template <int MODE, bool LGV>
+__global__ __launch_bounds__(256, 2) void end_conv_mfma_kernel(const float* __restrict__ in, const float* __restrict__ ss,
+                                                               const float* __restrict__ w, const float* __restrict__ bias,
+                                                               const float* __restrict__ sigmas,
+                                                               const int64_t* __restrict__ labels, float* __restrict__ out,
+                                                               int H, int W, LangevinArgs lg) {
+  constexpr int Cin = EC_CIN;
+  __shared__ float P[E2_NG * 16 * E2_PS];
+  __shared__ float sw[2 * Cin * 9];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = lane >> 4, l16 = lane & 15;
+  const int tiles_row = W / E2_TC, tiles_per_img = (H / E2_TR) * tiles_row;
+  const int b = blockIdx.x / tiles_per_img, tile = blockIdx.x % tiles_per_img;
+  const int y0 = (tile / tiles_row) * E2_TR, x0 = (tile % tiles_row) * E2_TC;
+  auto chan = [&](int ks, int j) { return 32 * ks + (j < 4 ? 4 * q + j : 12 + 4 * q + j); };
+
+  // raw input of one 16-pixel group: clamped addresses, unconditional loads (validity applied later)
+  auto load_group = [&](int g, float4 (&r)[8]) __attribute__((always_inline)) {
+    const int p = 16 * g + l16, pr = p / E2_PC, pc = p - pr * E2_PC;
+    const int yy = min(max(y0 - 1 + pr, 0), H - 1), xx = min(max(x0 - 1 + pc, 0), W - 1);
+    const float* src = in + (((size_t)b * H + yy) * W + xx) * Cin + 4 * q;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if constexpr (SDP_EC_KO & 4) {
+        r[2 * ks] = make_float4((float)g, (float)ks, 0.f, 1.f);
+        r[2 * ks + 1] = r[2 * ks];
+        continue;
+      }
+      r[2 * ks] = *reinterpret_cast<const float4*>(src + 32 * ks);
+      r[2 * ks + 1] = *reinterpret_cast<const float4*>(src + 32 * ks + 16);
+    }
+  };
+  float4 ra[8], rb[8];
+#if SDP_EC_DEPTH == 3
+  float4 rc[8];
+#endif
+  load_group(wave, ra);
+#if SDP_EC_DEPTH == 3
+  load_group(min(wave + 4, E2_NG - 1), rb);
+#endif
+
+  for (int i = tid; i < 2 * Cin * 9; i += 256) sw[i] = w[i];
+#if SDP_EC_SS_LDS
+  // (scale, shift) of the image's channels in LDS, read per group (frees 64 VGPRs for the load ring)
+  __shared__ __attribute__((aligned(16))) float4 ssl[Cin / 2];
+  if (tid < Cin / 2) ssl[tid] = reinterpret_cast<const float4*>(ss + (size_t)b * Cin * 2)[tid];
+  auto scale_shift = [&](int ks, int j) __attribute__((always_inline)) {
+    const float4 v = ssl[chan(ks, j) >> 1];
+    return (j & 1) ? make_float2(v.z, v.w) : make_float2(v.x, v.y);
+  };
+#else
+  float2 sc[4][8];
+  {
+    const float2* ssb = reinterpret_cast<const float2*>(ss) + (size_t)b * Cin;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sc[ks][j] = ssb[chan(ks, j)];
+  }
+  auto scale_shift = [&](int ks, int j) __attribute__((always_inline)) { return sc[ks][j]; };
+#endif
+  __syncthreads();
+  auto split8 = [](const float (&v)[8], bf16x8& hi, bf16x8& lo) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      hi[j] = (__bf16)v[j];
+      lo[j] = (__bf16)(v[j] - (float)hi[j]);
+    }
+  };
+  bf16x8 bh[4][2], bl[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int n = 16 * nb + l16, tap = n >> 1, co = n & 1;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = n < 18 ? sw[(co * Cin + chan(ks, j)) * 9 + tap] : 0.f;
+      split8(v, bh[ks][nb], bl[ks][nb]);
+    }
+
+  // ---- partials of the region's pixel groups (wave w takes groups w, w + 4, ...)
+  auto do_group = [&](int g, const float4 (&r)[8]) __attribute__((always_inline)) {
+    const int p = 16 * g + l16, pr = p / E2_PC, pc = p - pr * E2_PC;
+    const int yy = y0 - 1 + pr, xx = x0 - 1 + pc;
+    const bool ok = p < E2_NP && yy >= 0 && yy < H && xx >= 0 && xx < W;   // zero padding of the conv input
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float4 f0 = r[2 * ks], f1 = r[2 * ks + 1];
+      const float raw[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float2 sv = scale_shift(ks, j);
+        v[j] = ok ? ((SDP_EC_KO & 1) ? raw[j] : elu_max(fmaf(raw[j], sv.x, sv.y))) : 0.f;
+      }
+      bf16x8 ah, al;
+      split8(v, ah, al);
+      if constexpr (SDP_EC_KO & 2) {
+        acc0[ks] += (float)ah[0] + (float)al[1];
+        continue;
+      }
+      if constexpr (MODE == MODE_F32X3) {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks][0], acc0, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks][0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh[ks][1], acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl[ks][1], acc1, 0, 0, 0);
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh[ks][1], acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {   // C[pixel 4q + rr][column l16]
+      float* prow = P + (16 * g + 4 * q + rr) * E2_PS;
+      prow[l16] = acc0[rr];
+      if (l16 < 2) prow[16 + l16] = acc1[rr];
+    }
+  };
+  // two groups per iteration, each computed while the other's loads fly; the loads are unconditional
+  // (a clamped group index) so no branch join makes the compiler drain vmcnt
+#if SDP_EC_DEPTH == 3
+  for (int g = wave; g < E2_NG; g += 12) {   // ring of three: two groups' loads fly behind each compute
+    load_group(min(g + 8, E2_NG - 1), rc);
+    do_group(g, ra);
+    load_group(min(g + 12, E2_NG - 1), ra);
+    if (g + 4 < E2_NG) do_group(g + 4, rb);
+    load_group(min(g + 16, E2_NG - 1), rb);
+    if (g + 8 < E2_NG) do_group(g + 8, rc);
+  }
+#else
+  for (int g = wave; g < E2_NG; g += 8) {
+    load_group(min(g + 4, E2_NG - 1), rb);
+    do_group(g, ra);
+    load_group(min(g + 8, E2_NG - 1), ra);
+    if (g + 4 < E2_NG) do_group(g + 4, rb);
+  }
+#endif
+  __syncthreads();
+
+  // ---- out[r][c4 .. c4+3][co] = bias + sum over the 9 taps of the partials, / sigma
+  const int r = tid >> 4, co = (tid >> 3) & 1, c4 = (tid & 7) * 4;
+  float gv[4];
+  const float sg = sigmas[labels[b]], bco = bias[co];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float s = 0.f;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) s += P[((r + tap / 3) * E2_PC + c4 + k + tap % 3) * E2_PS + 2 * tap + co];
+    gv[k] = (s + bco) / sg;
+  }
+  const float4 g4 = make_float4(gv[0], gv[1], gv[2], gv[3]);
+  const size_t e = (((size_t)b * 2 + co) * H + y0 + r) * W + x0 + c4;
+  if constexpr (!LGV) {
+    *reinterpret_cast<float4*>(out + e) = g4;
+  } else {
+    if (out) *reinterpret_cast<float4*>(out + e) = g4;
+    float4 l;
+    const float4 o = langevin_group(lg, e / 4, g4, l);
+    reinterpret_cast<float4*>(lg.x)[e / 4] = o;
+    if (lg.lik) reinterpret_cast<float4*>(lg.lik)[e / 4] = l;
+    if (lg.absmax) block_absmax<4>(co == 0 ? absmax4(o) : 0u, lg.absmax);
   }
 }
 
@@ -510,9 +920,17 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
 
 // ---------------------------------------------------------------- host launchers
 hipError_t begin_conv(const float* x, const float* w, const float* bias, float* out, float* stats, int B, int H, int W,
-                      hipStream_t st) {
+                      hipStream_t st, int mode) {
   if (W % BC_TP) return hipErrorInvalidValue;
   const int ntiles = B * H * (W / BC_TP);
+  if (mode != MODE_F32 && !SDP_HEAD_DIRECT) {   // bf16 modes: the MFMA form
+    const dim3 grid(std::min(ntiles, 256 * BM_WG_PER_CU));
+    if (mode == MODE_F32X3)
+      hipLaunchKernelGGL(begin_conv_mfma_kernel<MODE_F32X3>, grid, dim3(256), 0, st, x, w, bias, out, stats, B, H, W);
+    else
+      hipLaunchKernelGGL(begin_conv_mfma_kernel<MODE_BF16>, grid, dim3(256), 0, st, x, w, bias, out, stats, B, H, W);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(begin_conv_kernel, dim3(std::min(ntiles, 256 * BC_WG_PER_CU)), dim3(256), 0, st, x, w, bias, out,
                      stats, B, H, W);
   return hipGetLastError();
@@ -520,8 +938,21 @@ hipError_t begin_conv(const float* x, const float* w, const float* bias, float* 
 
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st,
-                    const LangevinArgs* lg) {
-  if (Cin != EC_CIN || H % 4 || W % 64) return hipErrorInvalidValue;
+                    const LangevinArgs* lg, int mode) {
+  if (Cin != EC_CIN) return hipErrorInvalidValue;
+  if (mode != MODE_F32 && !SDP_HEAD_DIRECT && H % E2_TR == 0 && W % E2_TC == 0) {   // bf16 modes: the MFMA form
+    const dim3 grid(B * (H / E2_TR) * (W / E2_TC));
+    const LangevinArgs la = lg ? *lg : LangevinArgs{};
+    if (mode == MODE_F32X3) {
+      if (lg) hipLaunchKernelGGL((end_conv_mfma_kernel<MODE_F32X3, true>), grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W, la);
+      else hipLaunchKernelGGL((end_conv_mfma_kernel<MODE_F32X3, false>), grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W, la);
+    } else {
+      if (lg) hipLaunchKernelGGL((end_conv_mfma_kernel<MODE_BF16, true>), grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W, la);
+      else hipLaunchKernelGGL((end_conv_mfma_kernel<MODE_BF16, false>), grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W, la);
+    }
+    return hipGetLastError();
+  }
+  if (H % 4 || W % 64) return hipErrorInvalidValue;
   const dim3 grid(B * (H / 4) * (W / 64));
   if (lg)
     hipLaunchKernelGGL(end_conv_kernel<true>, grid, dim3(256), 0, st, in, ss, w, bias, sigmas, labels, out, H, W, *lg);

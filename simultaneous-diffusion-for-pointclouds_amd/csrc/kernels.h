@@ -7,11 +7,12 @@ namespace sdp {
 
 hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, const char** why);
 hipError_t begin_conv(const float* x, const float* w, const float* bias, float* out, float* stats, int B, int H, int W,
-                      hipStream_t st);
-// lg: fuse the Langevin update into the epilogue (out may then be null: scores not stored)
+                      hipStream_t st, int mode = MODE_F32);
+// lg: fuse the Langevin update into the epilogue (out may then be null: scores not stored); mode: the
+// conv arithmetic (MODE_F32: exact fp32 FMAs; bf16 modes: the MFMA partials form, fp32x3 / bf16)
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st,
-                    const LangevinArgs* lg = nullptr);
+                    const LangevinArgs* lg = nullptr, int mode = MODE_F32);
 // scratch: B*C*16 bytes (per-(b,c) float64 mean and variance)
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
                          const float* beta, float* ss, hipStream_t st, float* nst, void* scratch);

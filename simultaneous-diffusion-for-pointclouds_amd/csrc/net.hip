@@ -234,7 +234,7 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
   // begin_conv + input prep  -> FA (stats over 64-px tiles)
   f.prof_launch("begin_conv 4->128 @" + std::to_string(H) + "x" + std::to_string(W),
                 (double)B * H * W * (2 * 4 + C * 4) + (double)B * (H * W / 64) * C * 8, [&] {
-                  chk(begin_conv(x, net->P("begin_conv.weight"), net->P("begin_conv.bias"), FA.p, f.stats, B, H, W, st),
+                  chk(begin_conv(x, net->P("begin_conv.weight"), net->P("begin_conv.bias"), FA.p, f.stats, B, H, W, st, net->mode),
                       "begin_conv");
                 });
   // res1
@@ -301,7 +301,7 @@ static void forward_impl(sdp_net* net, const float* x, const int64_t* labels, fl
                     std::to_string(W),
                 (double)B * H * W * C * 4 + lg_bytes, [&] {
                   chk(end_conv(o.p, f.ss, net->P("end_conv.weight"), net->P("end_conv.bias"), net->P("sigmas"), labels,
-                               out, B, H, W, C, st, lg),
+                               out, B, H, W, C, st, lg, net->mode),
                       "end_conv");
                 });
 }

@@ -271,7 +271,7 @@ struct TrainPlan {
     mvs = take((size_t)B * 2 * C * 4);
     T4 x0 = mk(H, W, C);
     if (!dry)
-      ok(begin_conv(xin, P("begin_conv.weight"), P("begin_conv.bias"), x0.p, stats, B, H, W, st), "begin_conv");
+      ok(begin_conv(xin, P("begin_conv.weight"), P("begin_conv.bias"), x0.p, stats, B, H, W, st, net->mode), "begin_conv");
     T4 l1 = resf("res1.0", x0, false, 1, H * W / 64, 64.f);
     l1 = resf("res1.1", l1, false, 1, tiles(l1), 128.f);
     T4 l2 = resf("res2.0", l1, true, 1, tiles(l1), 128.f);
@@ -287,7 +287,7 @@ struct TrainPlan {
     norm("normalizer", tiles(o), 128.f, C);
     if (!dry)
       ok(end_conv(o.p, F("normalizer#ss"), P("end_conv.weight"), P("end_conv.bias"), P("sigmas"), lab, out, B, H, W, C,
-                  st),
+                  st, nullptr, net->mode),
          "end_conv");
     fwd_bytes = used;
   }
