@@ -22,6 +22,6 @@ step bench 600 python bench.py --steps 20 --warmup 3
 step bench_views8 600 python bench.py --steps 10 --warmup 2 --views 8 --no-cpu-baseline --no-fp32-line
 step bench_allforone 600 python bench.py --workload allforone --steps 10 --warmup 2
 step bench_train 600 python bench.py --workload train --steps 10 --warmup 2
-step rocprof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fp32-line
+step rocprof 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fp32-line --split 1
 step rocprof_train 600 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run --output-format csv -- python bench.py --workload train --steps 5 --warmup 1 --no-cpu-baseline
 exit 0
