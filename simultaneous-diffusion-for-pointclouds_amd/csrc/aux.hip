@@ -539,7 +539,13 @@ __global__ __launch_bounds__(256) void end_conv_kernel(const float* __restrict__
 // bound.  Lane l holds pixel l % 16 of a 16-pixel group and the 8 channels {4q..4q+3, 16+4q..16+4q+3}
 // (q = l / 16) of each 32-channel step -- two float4 loads; B uses the same channel order.
 // The (scale, shift) of the lane's 32 channels and the B fragments stay in registers for the block.
-constexpr int E2_TR = 16, E2_TC = 32, E2_PR = E2_TR + 2, E2_PC = E2_TC + 2, E2_NP = E2_PR * E2_PC;
+#ifndef SDP_EC_TR         // output tile of the MFMA end conv (rows x columns)
+#define SDP_EC_TR 16
+#endif
+#ifndef SDP_EC_TC
+#define SDP_EC_TC 32
+#endif
+constexpr int E2_TR = SDP_EC_TR, E2_TC = SDP_EC_TC, E2_PR = E2_TR + 2, E2_PC = E2_TC + 2, E2_NP = E2_PR * E2_PC;
 constexpr int E2_NG = (E2_NP + 15) / 16, E2_PS = 19;   // 16-pixel groups; P row stride (floats)
 #ifndef SDP_EC_DEPTH      // groups in the load ring (2 or 3)
 #define SDP_EC_DEPTH 2
@@ -689,28 +695,41 @@ __global__ __launch_bounds__(256, 2) void end_conv_mfma_kernel(const float* __re
 #endif
   __syncthreads();
 
-  // ---- out[r][c4 .. c4+3][co] = bias + sum over the 9 taps of the partials, / sigma
-  const int r = tid >> 4, co = (tid >> 3) & 1, c4 = (tid & 7) * 4;
-  float gv[4];
-  const float sg = sigmas[labels[b]], bco = bias[co];
+  // ---- out[r][c4 .. c4+3][co] = bias + sum over the 9 taps of the partials, / sigma; one float4
+  // group (4 columns of one row and channel) per thread and pass
+  constexpr int G4R = E2_TC / 4, NG4 = E2_TR * 2 * G4R, NPASS = (NG4 + 255) / 256;
+  const float sg = sigmas[labels[b]];
+  uint32_t lmax = 0u;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    float s = 0.f;
+  for (int pass = 0; pass < NPASS; ++pass) {
+    const int gi = tid + 256 * pass;
+    if (NG4 % 256 == 0 || gi < NG4) {
+      const int r = gi / (2 * G4R), co = (gi / G4R) & 1, c4 = (gi % G4R) * 4;
+      const float bco = bias[co];
+      float gv[4];
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) s += P[((r + tap / 3) * E2_PC + c4 + k + tap % 3) * E2_PS + 2 * tap + co];
-    gv[k] = (s + bco) / sg;
+      for (int k = 0; k < 4; ++k) {
+        float s = 0.f;
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) s += P[((r + tap / 3) * E2_PC + c4 + k + tap % 3) * E2_PS + 2 * tap + co];
+        gv[k] = (s + bco) / sg;
+      }
+      const float4 g4 = make_float4(gv[0], gv[1], gv[2], gv[3]);
+      const size_t e = (((size_t)b * 2 + co) * H + y0 + r) * W + x0 + c4;
+      if constexpr (!LGV) {
+        *reinterpret_cast<float4*>(out + e) = g4;
+      } else {
+        if (out) *reinterpret_cast<float4*>(out + e) = g4;
+        float4 l;
+        const float4 o = langevin_group(lg, e / 4, g4, l);
+        reinterpret_cast<float4*>(lg.x)[e / 4] = o;
+        if (lg.lik) reinterpret_cast<float4*>(lg.lik)[e / 4] = l;
+        if (co == 0) lmax = max(lmax, absmax4(o));
+      }
+    }
   }
-  const float4 g4 = make_float4(gv[0], gv[1], gv[2], gv[3]);
-  const size_t e = (((size_t)b * 2 + co) * H + y0 + r) * W + x0 + c4;
-  if constexpr (!LGV) {
-    *reinterpret_cast<float4*>(out + e) = g4;
-  } else {
-    if (out) *reinterpret_cast<float4*>(out + e) = g4;
-    float4 l;
-    const float4 o = langevin_group(lg, e / 4, g4, l);
-    reinterpret_cast<float4*>(lg.x)[e / 4] = o;
-    if (lg.lik) reinterpret_cast<float4*>(lg.lik)[e / 4] = l;
-    if (lg.absmax) block_absmax<4>(co == 0 ? absmax4(o) : 0u, lg.absmax);
+  if constexpr (LGV) {
+    if (lg.absmax) block_absmax<4>(lmax, lg.absmax);
   }
 }
 
