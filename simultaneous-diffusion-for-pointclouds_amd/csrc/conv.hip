@@ -4,6 +4,11 @@
 
 #include "conv_launch.h"
 
+// preferred tile width of the 128 px x 256 Cout workgroups (A/B knob): 32 = 4 x 32 tiles, 64 = 2 x 64
+#ifndef SDP_TC_WM1
+#define SDP_TC_WM1 32
+#endif
+
 namespace sdp {
 
 template <int MODE, bool PELU>
@@ -38,7 +43,13 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
 #else
   const int wm = (a.Cout % 256 == 0) ? 1 : 2;
 #endif
-  int tc = (wm == 2) ? 32 : ((Ws % 64 == 0) ? 64 : 32);
+  // 128 px x 256 Cout workgroups: 4 x 32 tiles (6 x 34 patch, 1.59x the pixels) where the sub-grid
+  // allows, else 2 x 64 (4 x 66 patch, 2.06x) -- 4 x 32 measured 171.4 -> 167.0 us per 256->256
+  // @32x512 launch (profiles/experiments/r02_tile_width_ab.log)
+  const int tpref = SDP_TC_WM1, talt = tpref == 32 ? 64 : 32;
+  int tc = (wm == 2) ? 32
+                     : ((Ws % tpref == 0 && Hs % (128 / tpref) == 0) ? tpref
+                                                                     : ((Ws % talt == 0 && Hs % (128 / talt) == 0) ? talt : 32));
 #ifdef SDP_CONV_BENCH_ONLY   // SDP_TC=32|64 forces the tile width of the WM=1 shape
   if (wm == 1 && getenv("SDP_TC")) tc = atoi(getenv("SDP_TC"));
 #endif

@@ -10,6 +10,12 @@
 
 #include "conv_launch.h"
 
+// preferred tile width of the 128 px x 256 Cout data-gradient workgroups (A/B knob; the forward's is
+// SDP_TC_WM1 in conv.hip)
+#ifndef SDP_DGRAD_TC_WM1
+#define SDP_DGRAD_TC_WM1 64
+#endif
+
 namespace sdp {
 
 template <int MODE>
@@ -29,7 +35,10 @@ hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char**
   if (a.pro_mode != PRO_NONE || a.up || a.out2 || a.stats) { *why = "dgrad: plain input, no fused extras"; return hipErrorInvalidValue; }
   const int Hs = a.H / d, Ws = a.W / d;
   const int wm = (a.Cout % 256 == 0 && ks == 3 && a.circular) ? 1 : 2;
-  const int tc = (wm == 2) ? 32 : ((Ws % 64 == 0) ? 64 : 32);
+  const int tpref = SDP_DGRAD_TC_WM1, talt = tpref == 32 ? 64 : 32;
+  const int tc = (wm == 2) ? 32
+                           : ((Ws % tpref == 0 && Hs % (128 / tpref) == 0) ? tpref
+                                                                           : ((Ws % talt == 0 && Hs % (128 / talt) == 0) ? talt : 32));
   const int tr = wm * 128 / tc;
   if (Ws % tc || Hs % tr) { *why = "dgrad: sub-grid not divisible by the pixel tile"; return hipErrorInvalidValue; }
   if (!a.circular && d != 1) { *why = "dgrad: zero padding only for d=1"; return hipErrorInvalidValue; }
