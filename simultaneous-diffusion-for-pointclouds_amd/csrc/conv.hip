@@ -4,9 +4,14 @@
 
 #include "conv_launch.h"
 
-// preferred tile width of the 128 px x 256 Cout workgroups (A/B knob): 32 = 4 x 32 tiles, 64 = 2 x 64
+// preferred tile width of the 128 px x 256 Cout workgroups (A/B knob): 32 = 4 x 32 tiles, 64 = 2 x 64,
+// 16 = 8 x 16 (bf16 modes on the 16x16 shape only)
 #ifndef SDP_TC_WM1
-#define SDP_TC_WM1 32
+#define SDP_TC_WM1 16
+#endif
+// tile width of the 256 px x 128 Cout workgroups: 32 = 8 x 32 tiles, 16 = 16 x 16 (16x16 shape only)
+#ifndef SDP_TC_WM2
+#define SDP_TC_WM2 32
 #endif
 
 namespace sdp {
@@ -15,6 +20,9 @@ template <int MODE, bool PELU>
 static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
   if (ks == 1) return conv_launch<MODE, 1, 64, 1, true, PELU>(a, st);   // only the ConvMeanPool 1x1 shortcut
   if (pool) return conv_launch<MODE, 1, 64, 3, true, PELU>(a, st);
+  if constexpr (MODE != MODE_F32) {   // 16-wide tiles: the 16x16 MFMA shape only
+    if (tc == 16) return wm == 2 ? conv_launch<MODE, 2, 16, 3, false, PELU>(a, st) : conv_launch<MODE, 1, 16, 3, false, PELU>(a, st);
+  }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, PELU>(a, st);
   return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, PELU>(a, st) : conv_launch<MODE, 1, 32, 3, false, PELU>(a, st);
 }
@@ -46,8 +54,11 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   // 128 px x 256 Cout workgroups: 4 x 32 tiles (6 x 34 patch, 1.59x the pixels) where the sub-grid
   // allows, else 2 x 64 (4 x 66 patch, 2.06x) -- 4 x 32 measured 171.4 -> 167.0 us per 256->256
   // @32x512 launch (profiles/experiments/r02_tile_width_ab.log)
-  const int tpref = SDP_TC_WM1, talt = tpref == 32 ? 64 : 32;
-  int tc = (wm == 2) ? 32
+  // 16-wide tiles exist for the 16x16 MFMA shape (bf16 modes) only
+  const bool sh16 = mode != MODE_F32 && !getenv("SDP_MFMA_SHAPE");
+  const int tpref = (SDP_TC_WM1 == 16 && !sh16) ? 32 : SDP_TC_WM1;
+  const int talt = tpref == 32 ? 64 : 32;
+  int tc = (wm == 2) ? ((SDP_TC_WM2 == 16 && sh16 && Ws % 16 == 0 && Hs % 16 == 0) ? 16 : 32)
                      : ((Ws % tpref == 0 && Hs % (128 / tpref) == 0) ? tpref
                                                                      : ((Ws % talt == 0 && Hs % (128 / talt) == 0) ? talt : 32));
 #ifdef SDP_CONV_BENCH_ONLY   // SDP_TC=32|64 forces the tile width of the WM=1 shape

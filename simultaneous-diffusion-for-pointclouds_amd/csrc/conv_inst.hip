@@ -43,8 +43,11 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st) {
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
-  return hipGetLastError();
+  if constexpr (TC >= 32) {   // the 32x32 shape tiles rows in 32-pixel fragments
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;   // (not reached: conv.hip picks 16-wide tiles for the 16x16 forward only)
 }
 
 template <int MODE, int WM, int TC, int KS, bool ZP>
@@ -67,6 +70,8 @@ template <> struct FwdShape<1> { static constexpr int WM = 1, TC = 64, KS = 3; s
 template <> struct FwdShape<2> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool POOL = false; };
 template <> struct FwdShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool POOL = false; };
 template <> struct FwdShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool POOL = false; };
+template <> struct FwdShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
+template <> struct FwdShape<6> { static constexpr int WM = 2, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
 template <int S> struct DgradShape;
 template <> struct DgradShape<0> { static constexpr int WM = 2, TC = 32, KS = 1; static constexpr bool ZP = false; };
 template <> struct DgradShape<1> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool ZP = true; };
@@ -76,7 +81,8 @@ template <> struct DgradShape<4> { static constexpr int WM = 1, TC = 32, KS = 3;
 
 #if defined(SDP_INST) && SDP_INST < 1000
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
-static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && kShape <= 4, "SDP_INST: bad forward code");
+static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && kShape <= 6 && (kShape < 5 || kMode != MODE_F32),
+              "SDP_INST: bad forward code");
 using FS = FwdShape<kShape>;
 template hipError_t conv_launch<kMode, FS::WM, FS::TC, FS::KS, FS::POOL, (kPelu != 0)>(ConvArgs, hipStream_t);
 #elif defined(SDP_INST)

@@ -612,6 +612,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
       }
     });
   } else if (a.dact) {
+    if constexpr (TC >= 32) {   // (TC = 16 tiles are forward-only, 16x16 shape)
     // data-gradient launches (training): the LDS-staged epilogue -- its 16-B pixel-row
     // accesses of the elu' operand and the residual gradient beat per-channel 4-B accesses
     // ------------------------------------------------------------------ epilogue
@@ -795,7 +796,9 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         *st = make_float2(mean, m2);
       }
     }
+    }  // if constexpr (TC >= 32)
   } else {
+    if constexpr (SH == 32) {   // the 32x32 direct epilogue (the 16x16 forward takes the first branch)
     // ------------------------------------------------------------------ epilogue
     // Straight from the accumulators, no LDS round trip: register r of fragment (mb, nb) of
     // lane l holds pixel m = (r&3) + 8(r>>2) + 4(l>>5) of the fragment's 32-pixel row segment
@@ -933,6 +936,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         }
       });
     }
+    }  // if constexpr (SH == 32)
   }
 #ifdef SDP_TIMING
   SDP_T(4);
