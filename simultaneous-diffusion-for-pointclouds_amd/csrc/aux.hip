@@ -810,11 +810,11 @@ __global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict
 
 // ---------------------------------------------------------------- maxpool 5x5 s1 p2 (NHWC)
 // Block = a strip of MP_COLS columns x 128 channels (32 float4 lanes per pixel, so a wave reads
-// two whole 512-B pixel rows) over MP_ROWS output rows.  Each input row of the strip plus its 2+2
+// two whole 512-B pixel rows) over `rows` output rows.  Each input row of the strip plus its 2+2
 // halo columns is landed in LDS ONCE by LDS-DMA, MP_D rows ahead of its use in a ring of MP_NS
 // row slots; every thread takes the 5-wide horizontal max of its (column, 4 channels) from LDS and
 // slides a 5-row window of those maxima in registers -> per output (MP_COLS+4)/MP_COLS x
-// (MP_ROWS+4)/MP_ROWS global reads.  One barrier per row.  The DMA has no register result, so the
+// (rows+4)/rows global reads.  One barrier per row.  The DMA has no register result, so the
 // compiler places no wait for it: each thread waits for its own DMA of a row with an explicit
 // vmcnt (vector memory ops retire in order on gfx9, and exactly P DMAs + S stores per row follow).
 // Out-of-image rows/columns are read at the clamped (edge) position: a copy of a value that is
@@ -824,10 +824,17 @@ __global__ __launch_bounds__(1024) void inpp_ss_kernel(const double2* __restrict
 // max_pool2d keeps for its backward.  For it the edge copies are overwritten with -inf (an edge
 // copy sits earlier in window order than its original and would take the tie), so -inf padding
 // never wins.
-constexpr int MP_ROWS = 16, MP_COLS = 8, MP_NS = 6, MP_D = 2;
+// output rows per block: 32 while the grid keeps >= MP_MIN_BLOCKS blocks, else 16 -- 256 @32x512
+// (512 blocks either way) 35.5 -> 27.3 us, 128 @64x1024 58.4 -> 57 us; 128 @32x512 would drop to 256
+// blocks and run 19.1 -> 23.2 us, so it keeps 16 (profiles/experiments/r02_maxpool_rows_ab.log)
+#ifndef SDP_MP_MIN_BLOCKS
+#define SDP_MP_MIN_BLOCKS 512
+#endif
+constexpr int MP_COLS = 8, MP_NS = 6, MP_D = 2, MP_MIN_BLOCKS = SDP_MP_MIN_BLOCKS;
 template <bool IDX>
 __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                       uchar4* __restrict__ idx, int B, int H, int W, int C) {
+                                                       uchar4* __restrict__ idx, int B, int H, int W, int C,
+                                                       int rows) {
   constexpr int SC = MP_COLS + 4;                  // staged columns
   constexpr int NUNIT = SC * 32;                   // float4 units per staged row: 384 = waves 0..3 + waves 0..1
   static_assert(NUNIT == 384 && MP_NS >= MP_D + 1 && 4 + MP_D <= MP_NS, "maxpool5 ring layout");
@@ -835,7 +842,7 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
   const int tid = threadIdx.x, c4 = tid & 31, xl = tid >> 5;   // (column in strip, float4 channel group)
   const int wave = tid >> 6;
   const int C4 = C / 4, CG = C4 / 32;              // 128-channel groups
-  const int strips = W / MP_COLS, RB = (H + MP_ROWS - 1) / MP_ROWS;
+  const int strips = W / MP_COLS, RB = (H + rows - 1) / rows;
   // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so give each XCD a contiguous
   // range -- the strips on either side of a strip (its halo columns) then sit in the same L2
   const int nwg = gridDim.x;
@@ -845,7 +852,7 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
   const int strip = t % strips;
   t /= strips;
   const int rb = t % RB, b = t / RB;
-  const int x0 = strip * MP_COLS, y0 = rb * MP_ROWS, y1 = min(H, y0 + MP_ROWS);
+  const int x0 = strip * MP_COLS, y0 = rb * rows, y1 = min(H, y0 + rows);
   const int x = x0 + xl;
   const float NEG = -INFINITY;
   const i32x4 rs = buffer_desc(in + (size_t)b * H * W * C, (uint32_t)H * W * C * 4);
@@ -994,12 +1001,13 @@ hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, con
 
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
   if (C % 128 || W % MP_COLS) return hipErrorInvalidValue;
-  const int grid = B * ((H + MP_ROWS - 1) / MP_ROWS) * (W / MP_COLS) * (C / 128);
+  auto blocks = [&](int rows) { return B * ((H + rows - 1) / rows) * (W / MP_COLS) * (C / 128); };
+  const int rows = blocks(32) >= MP_MIN_BLOCKS ? 32 : 16, grid = blocks(rows);
   if (idx)
     hipLaunchKernelGGL(maxpool5_kernel<true>, dim3(grid), dim3(256), 0, st, in, out, reinterpret_cast<uchar4*>(idx), B, H,
-                       W, C);
+                       W, C, rows);
   else
-    hipLaunchKernelGGL(maxpool5_kernel<false>, dim3(grid), dim3(256), 0, st, in, out, nullptr, B, H, W, C);
+    hipLaunchKernelGGL(maxpool5_kernel<false>, dim3(grid), dim3(256), 0, st, in, out, nullptr, B, H, W, C, rows);
   return hipGetLastError();
 }
 
