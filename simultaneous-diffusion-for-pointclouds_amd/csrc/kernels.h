@@ -54,7 +54,10 @@ hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow,
 hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char** why);
 // weight-gradient workgroups per launch (pixel splits x Cin/32 x Cout/128): one round of
 // two workgroups per CU (1024: +2% kernel time and a costlier reduce)
-constexpr int WGRAD_TARGET_BLOCKS = 512;
+#ifndef SDP_WGRAD_BLOCKS   // weight-gradient workgroups aimed for per launch (pixel splits x channel blocks)
+#define SDP_WGRAD_BLOCKS 512
+#endif
+constexpr int WGRAD_TARGET_BLOCKS = SDP_WGRAD_BLOCKS;
 int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks);
 size_t wgrad_part_floats(int S, int Cin, int Cout, int ks);
 hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,
