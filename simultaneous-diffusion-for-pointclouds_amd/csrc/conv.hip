@@ -3,6 +3,7 @@
 #include <cstdlib>
 
 #include "conv_launch.h"
+#include "wino_launch.h"
 
 // preferred tile width of the 128 px x 256 Cout workgroups (A/B knob): 32 = 4 x 32 tiles, 64 = 2 x 64,
 // 16 = 8 x 16 (bf16 modes on the 16x16 shape only)
@@ -38,9 +39,33 @@ static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int 
 #endif
 }
 
+// Winograd F(2,3) path (wino_kernel.h): the circular 3x3 non-pooled forward convs in the bf16 modes
+// whose sub-grid tiles into 8 x 16 pixels.  SDP_WINO (bit mask, default 3): 1 = 256-channel outputs
+// (128 px x 256 Cout workgroups), 2 = 128-channel outputs (128 px x 128 Cout); 0 = direct only
+// (default while the Winograd kernel is slower than the direct one).
+static int wino_mask() {
+  static const int m = [] {
+    const char* e = getenv("SDP_WINO");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
+
+template <int MODE>
+static hipError_t wino_mode(const ConvArgs& a, int wm, hipStream_t st) {
+  if (wm == 1) return a.pro_mode == PRO_NONE ? wino_launch<MODE, 1, false>(a, st) : wino_launch<MODE, 1, true>(a, st);
+  return a.pro_mode == PRO_NONE ? wino_launch<MODE, 2, false>(a, st) : wino_launch<MODE, 2, true>(a, st);
+}
+
 // Host entry: validates the shape contract the kernel's indexing assumes, then launches.
 hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, const char** why) {
   const int d = a.dil;
+  if (a.wfw && mode != MODE_F32 && ks == 3 && !pool && a.circular && !a.dact && a.Cin % 64 == 0 && a.H % d == 0 &&
+      a.W % d == 0 && (a.H / d) % 8 == 0 && (a.W / d) % 16 == 0 && a.pro_ss &&
+      (a.Cin <= 1024 || a.ss_bstride != 0)) {
+    const int wm = a.Cout % 256 == 0 ? 1 : (a.Cout % 128 == 0 ? 2 : 0);
+    if (wm && (wino_mask() & wm)) return mode == MODE_F32X3 ? wino_mode<MODE_F32X3>(a, wm, st) : wino_mode<MODE_BF16>(a, wm, st);
+  }
   if (a.Cin % 64 || a.Cout % 128) { *why = "conv: Cin%64 and Cout%128 required"; return hipErrorInvalidValue; }
   if (a.H % d || a.W % d) { *why = "conv: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
   const int Hs = a.H / d, Ws = a.W / d;

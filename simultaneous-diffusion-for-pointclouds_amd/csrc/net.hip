@@ -53,6 +53,7 @@ struct Fwd {
     ConvArgs a{};
     a.in = in.p;
     a.wf = reinterpret_cast<const uint4*>(net->P(wkey + ".weight#frag"));
+    a.wfw = net->wino_w(wkey);
     a.bias = o.bias ? net->P(wkey + ".bias") : nullptr;
     a.out = out.p;
     a.res = o.res;

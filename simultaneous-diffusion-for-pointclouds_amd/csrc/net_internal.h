@@ -123,6 +123,10 @@ struct sdp_net {
     if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
     return e;
   }
+  const uint4* wino_w(const std::string& wkey) const {   // "#wfrag" of a 3x3 conv, or null
+    auto it = dev.find(wkey + ".weight#wfrag");
+    return it == dev.end() ? nullptr : reinterpret_cast<const uint4*>(it->second);
+  }
   const float* P(const std::string& k) const {
     auto it = dev.find(k);
     if (it == dev.end()) throw std::runtime_error("missing parameter " + k);
@@ -148,17 +152,22 @@ struct sdp_net {
     for (auto& kv : host) {
       if (!is_conv_w(kv.first)) continue;
       const auto& s = kv.second.shape;
-      const size_t bytes = kv.second.data.size() * 4;
-      for (int dg = 0; dg < (train_packs ? 2 : 1); ++dg) {
-        const std::string fk = kv.first + (dg ? "#dfrag" : "#frag");
+      // packings: 0 = forward "#frag", 1 = data gradient "#dfrag" (training), 2 = the Winograd
+      // F(2,3) forward "#wfrag" of the 3x3 convs (bf16 modes; 12 transformed taps)
+      for (int dg = 0; dg < 3; ++dg) {
+        if (dg == 1 && !train_packs) continue;
+        if (dg == 2 && (s[2] != 3 || mode == sdp::MODE_F32)) continue;
+        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 1 ? "#dfrag" : "#wfrag");
+        const int nt = dg == 2 ? 12 : (int)(s[2] * s[3]);
+        const size_t n = (size_t)s[0] * s[1] * nt;
         if (!dev.count(fk)) {
           void* p = nullptr;
-          sdp::chk(hipMalloc(&p, bytes), "hipMalloc");
+          sdp::chk(hipMalloc(&p, n * 4), "hipMalloc");
           dev[fk] = p;
         }
-        d.push_back(sdp::PackDesc{P(kv.first), reinterpret_cast<uint32_t*>(dev[fk]), (int)s[0], (int)s[1],
-                                  (int)(s[2] * s[3]), dg, total});
-        total += kv.second.data.size();
+        d.push_back(sdp::PackDesc{P(kv.first), reinterpret_cast<uint32_t*>(dev[fk]), (int)s[0], (int)s[1], nt, dg,
+                                  total});
+        total += n;
       }
     }
     const bool same = d.size() == pack_host.size() &&

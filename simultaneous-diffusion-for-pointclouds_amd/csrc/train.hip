@@ -98,6 +98,7 @@ struct TrainPlan {
     ConvArgs a{};
     a.in = in.p;
     a.wf = reinterpret_cast<const uint4*>(P(wkey + ".weight#frag"));
+    a.wfw = net->wino_w(wkey);
     a.bias = o.bias ? P(wkey + ".bias") : nullptr;
     a.out = out.p;
     a.res = o.res;

@@ -56,6 +56,34 @@ SDP_DEV uint32_t pack_slot(const float* __restrict__ w, int Cout, int Cin, int N
   return pk;
 }
 
+// Winograd F(2,3)-along-W packing consumed by wino_conv_kernel (wino_kernel.h):
+// [chunk = Cin/32][tap = 4 kh + j][nf = Cout/16][lane 64][8 slots of 4 B: hi x 4 | lo x 4]
+// lane l: Cout nf*16 + l%16, channels chunk*32 + 8(l/16) + 0..7 (two bf16 per slot), of
+// U_j[kh] = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)[j] over the kernel row g = w[co][ci][kh][0..2]
+SDP_DEV uint32_t pack_slot_wino(const float* __restrict__ w, int Cout, int Cin, int mode, size_t i) {
+  const int NF = Cout / 16;
+  const int slot = i & 7;
+  size_t r = i >> 3;
+  const int lane = r & 63;
+  r >>= 6;
+  const int nf = r % NF;
+  r /= NF;
+  const int tap = r % 12;
+  const int ch = r / 12;
+  const int co = nf * 16 + (lane & 15), kh = tap >> 2, j = tap & 3;
+  const int hl = slot >> 2, e0 = (slot & 3) * 2;
+  uint32_t pk = 0;
+  for (int e = 0; e < 2; ++e) {
+    const int ci = ch * 32 + 8 * (lane >> 4) + e0 + e;
+    const float* g = w + ((size_t)co * Cin + ci) * 9 + kh * 3;
+    const float u = j == 0 ? g[0] : j == 3 ? g[2] : j == 1 ? 0.5f * ((g[0] + g[1]) + g[2]) : 0.5f * ((g[0] - g[1]) + g[2]);
+    const __bf16 hi = (__bf16)u;
+    const __bf16 q = (hl && mode == MODE_F32X3) ? (__bf16)(u - (float)hi) : hi;
+    pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
+  }
+  return pk;
+}
+
 __global__ void pack_weights_kernel(const float* __restrict__ w, uint32_t* __restrict__ out, int Cout, int Cin, int NT,
                                     int mode, int dgrad) {
   const size_t n = (size_t)Cout * Cin * NT;    // output 32-bit slots
@@ -69,7 +97,7 @@ __global__ void pack_weights_multi_kernel(const PackDesc* __restrict__ d, int mo
   const PackDesc e = d[blockIdx.y];
   const size_t n = (size_t)e.Cout * e.Cin * e.NT;
   for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x)
-    e.out[j] = pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
+    e.out[j] = e.dgrad == 2 ? pack_slot_wino(e.w, e.Cout, e.Cin, mode, j) : pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
 }
 
 hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st) {

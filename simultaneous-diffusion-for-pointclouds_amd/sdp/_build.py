@@ -4,7 +4,9 @@ The shared library is a build artefact (git-ignored), so a fresh checkout has no
 compiles it with the csrc Makefile when it is missing or when the sources changed since it was
 built, and raises with the compiler's output if that fails. "Changed" is decided by a content
 hash of every csrc file and include/sdp.h, written next to the library as ``libsdp.so.stamp``
-(mtimes are not trusted: a tree copied to another machine may carry arbitrary ones).
+(mtimes are not trusted: a tree copied to another machine may carry arbitrary ones -- so a
+rebuild is ``make -B``, which recompiles every object whatever its mtime; ``write_stamp()`` marks
+a library built by hand with ``make`` in csrc/ as current, for the edit-build loop).
 
 A lock file serialises concurrent callers (e.g. several ranks of one job starting together).
 This module imports neither torch nor the library, so it is safe to call before any GPU work.
@@ -58,6 +60,14 @@ def _stamp_ok(digest: str) -> bool:
         return fh.read().strip() == digest
 
 
+def write_stamp() -> None:
+    """Mark the current libsdp.so as built from the current sources (after a manual ``make``)."""
+    if not os.path.exists(LIB_PATH):
+        raise FileNotFoundError(LIB_PATH)
+    with open(STAMP, "w") as fh:
+        fh.write(source_hash() + "\n")
+
+
 def ensure_built(force_make: bool = False, verbose: bool = True) -> str:
     """Return the library path, building it first if it is missing or stale."""
     if "SDP_LIB" in os.environ:          # an explicitly provided library is used as is
@@ -74,7 +84,7 @@ def ensure_built(force_make: bool = False, verbose: bool = True) -> str:
             jobs = str(max(1, min(16, os.cpu_count() or 4)))
             if verbose:
                 print(f"[sdp] building libsdp.so (make -j{jobs} in {CSRC})", file=sys.stderr, flush=True)
-            p = subprocess.Popen(["make", "-j", jobs, "-C", CSRC], stdout=subprocess.PIPE,
+            p = subprocess.Popen(["make", "-B", "-j", jobs, "-C", CSRC], stdout=subprocess.PIPE,
                                  stderr=subprocess.STDOUT, text=True)
             log = []
             for line in p.stdout:
