@@ -61,6 +61,7 @@ SDP_DEV float elu_grad(float t, int form) {
 struct ConvArgs {
   const float* in;         // [B][H][W][Cin]
   const uint4* wf;         // fragment-ordered weights (see net.cpp pack_conv_weights)
+  const uint4* wf16;       // forward weights in 16x16 fragment order (train_aux.hip pack_slot16), or null
   const uint4* wfw;        // Winograd F(2,3)-transformed weights in 16x16 fragment order (wino_kernel.h), or null
   const float* bias;       // [Cout] or null
   float* out;              // [B][Ho][Wo][Cout]  (Ho,Wo = H,W or H/2,W/2 when pooled)

@@ -148,7 +148,11 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
 
   // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
   // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wf, 0, 0x7fffffff, 0x00020000);
+  // SH 16 forward: the 16x16-native packing "#frag16" when present (every fragment load of a wave
+  // reads 1 KiB contiguous), else the 32x32 packing read in 16-B pieces per lane
+  const bool c16 = SH == 16 && !a.dact && a.wf16;
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(c16 ? a.wf16 : a.wf), 0, 0x7fffffff, 0x00020000);
   const int wv0 = ((nbg0 + 0) * 64 + lane) * 64, wv1 = ((nbg0 + 1) * 64 + lane) * 64;
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
   // weight fragment ring: 3 taps deep (prefetch distance 2) when the tap count is a multiple
@@ -159,12 +163,14 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   // channel group g = l / 16 (channels 8g .. 8g+7 of the chunk); the 32x32 packing stores Cout c,
   // channels 16 s + 8 h at lane c % 32 + 32 h, slot s -- so the lane reads from there
   int wq16[4];
+  const int wlo16 = __builtin_amdgcn_readfirstlane(c16 ? 1024 : 16);   // byte offset of the lo part
   {
     const int g = lane >> 4, h = g & 1, sg = g >> 1;
     static_for<0, 4>([&](auto njc) {
       constexpr int nj = decltype(njc)::value;
       const int L = 16 * (nj & 1) + (lane & 15) + 32 * h;
-      wq16[nj] = ((nbg0 + (nj >> 1)) * 64 + L) * 64 + sg * 32;
+      // "#frag16": [chunk][tap][16-Cout fragment][hi, lo][lane][16 B]
+      wq16[nj] = c16 ? ((nbg0 * 2 + nj) * 128 + lane) * 16 : ((nbg0 + (nj >> 1)) * 64 + L) * 64 + sg * 32;
     });
   }
   auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
@@ -187,7 +193,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
         const u32x4 vh = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj], so, 0);
         bq[J][nj >> 1][2 * (nj & 1)] = make_uint4(vh.x, vh.y, vh.z, vh.w);
         if constexpr (MODE != MODE_BF16) {
-          const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj] + 16, so, 0);
+          const u32x4 vl = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj] + wlo16, so, 0);
           bq[J][nj >> 1][2 * (nj & 1) + 1] = make_uint4(vl.x, vl.y, vl.z, vl.w);
         }
       });

@@ -54,6 +54,7 @@ struct Fwd {
     a.in = in.p;
     a.wf = reinterpret_cast<const uint4*>(net->P(wkey + ".weight#frag"));
     a.wfw = net->wino_w(wkey);
+    a.wf16 = getenv("SDP_FRAG16") && atoi(getenv("SDP_FRAG16")) == 0 ? nullptr : net->frag16_w(wkey);
     a.bias = o.bias ? net->P(wkey + ".bias") : nullptr;
     a.out = out.p;
     a.res = o.res;

@@ -127,6 +127,10 @@ struct sdp_net {
     auto it = dev.find(wkey + ".weight#wfrag");
     return it == dev.end() ? nullptr : reinterpret_cast<const uint4*>(it->second);
   }
+  const uint4* frag16_w(const std::string& wkey) const {   // "#frag16" (bf16 modes), or null
+    auto it = dev.find(wkey + ".weight#frag16");
+    return it == dev.end() ? nullptr : reinterpret_cast<const uint4*>(it->second);
+  }
   const float* P(const std::string& k) const {
     auto it = dev.find(k);
     if (it == dev.end()) throw std::runtime_error("missing parameter " + k);
@@ -153,11 +157,13 @@ struct sdp_net {
       if (!is_conv_w(kv.first)) continue;
       const auto& s = kv.second.shape;
       // packings: 0 = forward "#frag", 1 = data gradient "#dfrag" (training), 2 = the Winograd
-      // F(2,3) forward "#wfrag" of the 3x3 convs (bf16 modes; 12 transformed taps)
-      for (int dg = 0; dg < 3; ++dg) {
+      // F(2,3) forward "#wfrag" of the 3x3 convs (bf16 modes; 12 transformed taps), 3 = the forward
+      // in 16x16 fragment order "#frag16" (bf16 modes)
+      for (int dg = 0; dg < 4; ++dg) {
         if (dg == 1 && !train_packs) continue;
         if (dg == 2 && (s[2] != 3 || mode == sdp::MODE_F32)) continue;
-        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 1 ? "#dfrag" : "#wfrag");
+        if (dg == 3 && mode == sdp::MODE_F32) continue;
+        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 1 ? "#dfrag" : dg == 2 ? "#wfrag" : "#frag16");
         const int nt = dg == 2 ? 12 : (int)(s[2] * s[3]);
         const size_t n = (size_t)s[0] * s[1] * nt;
         if (!dev.count(fk)) {

@@ -56,25 +56,52 @@ SDP_DEV uint32_t pack_slot(const float* __restrict__ w, int Cout, int Cin, int N
   return pk;
 }
 
-// Winograd F(2,3)-along-W packing consumed by wino_conv_kernel (wino_kernel.h):
-// [chunk = Cin/32][tap = 4 kh + j][nf = Cout/16][lane 64][8 slots of 4 B: hi x 4 | lo x 4]
-// lane l: Cout nf*16 + l%16, channels chunk*32 + 8(l/16) + 0..7 (two bf16 per slot), of
-// U_j[kh] = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)[j] over the kernel row g = w[co][ci][kh][0..2]
-SDP_DEV uint32_t pack_slot_wino(const float* __restrict__ w, int Cout, int Cin, int mode, size_t i) {
+// 16x16 fragment order of the forward (conv_mfma_kernel SH = 16): [chunk][tap][nf = Cout/16][hl][lane 64]
+// [4 words = 8 bf16]; lane l: Cout nf*16 + l%16, channels chunk*32 + 8 (l/16) + 0..7 (hl: hi / lo part),
+// so every fragment load of a wave reads 1 KiB contiguous
+SDP_DEV uint32_t pack_slot16(const float* __restrict__ w, int Cout, int Cin, int NT, int mode, size_t i) {
   const int NF = Cout / 16;
-  const int slot = i & 7;
-  size_t r = i >> 3;
-  const int lane = r & 63;
-  r >>= 6;
+  const int word = i & 3;
+  const int lane = (i >> 2) & 63;
+  const int hl = (i >> 8) & 1;
+  size_t r = i >> 9;
   const int nf = r % NF;
   r /= NF;
-  const int tap = r % 12;
-  const int ch = r / 12;
-  const int co = nf * 16 + (lane & 15), kh = tap >> 2, j = tap & 3;
-  const int hl = slot >> 2, e0 = (slot & 3) * 2;
+  const int tap = r % NT;
+  const int ch = r / NT;
+  const int co = nf * 16 + (lane & 15);
   uint32_t pk = 0;
   for (int e = 0; e < 2; ++e) {
-    const int ci = ch * 32 + 8 * (lane >> 4) + e0 + e;
+    const int ci = ch * 32 + 8 * (lane >> 4) + word * 2 + e;
+    const float f = w[((size_t)co * Cin + ci) * NT + tap];
+    const __bf16 hi = (__bf16)f;
+    const __bf16 q = (hl && mode == MODE_F32X3) ? (__bf16)(f - (float)hi) : hi;
+    pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
+  }
+  return pk;
+}
+
+// Winograd F(2,3)-along-W packing consumed by wino_conv_kernel (wino_kernel.h), 32x32x16 fragments
+// over 12 transformed taps, tap = 4 kh + j, of U_j[kh] = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)[j] over
+// the kernel row g = w[co][ci][kh][0..2]:
+//   [chunk = Cin/32][tap 12][nb = Cout/32][q = 2 s + hl, 4][lane 64][4 words: 8 bf16]
+// lane l holds Cout nb*32 + l%32, channels chunk*32 + 16 s + 8 (l/32) + 0..7 (hl: hi / lo part), so
+// each 16-B-per-lane fragment load of a wave reads 1 KiB contiguous
+SDP_DEV uint32_t pack_slot_wino(const float* __restrict__ w, int Cout, int Cin, int mode, size_t i) {
+  const int NB = Cout / 32;
+  const int word = i & 3;
+  const int lane = (i >> 2) & 63;
+  const int q = (i >> 8) & 3;
+  size_t r = i >> 10;
+  const int nb = r % NB;
+  r /= NB;
+  const int tap = r % 12;
+  const int ch = r / 12;
+  const int s = q >> 1, hl = q & 1, j0 = word * 2;
+  const int co = nb * 32 + (lane & 31), kh = tap >> 2, j = tap & 3;
+  uint32_t pk = 0;
+  for (int e = 0; e < 2; ++e) {
+    const int ci = ch * 32 + 16 * s + 8 * (lane >> 5) + j0 + e;
     const float* g = w + ((size_t)co * Cin + ci) * 9 + kh * 3;
     const float u = j == 0 ? g[0] : j == 3 ? g[2] : j == 1 ? 0.5f * ((g[0] + g[1]) + g[2]) : 0.5f * ((g[0] - g[1]) + g[2]);
     const __bf16 hi = (__bf16)u;
@@ -97,7 +124,9 @@ __global__ void pack_weights_multi_kernel(const PackDesc* __restrict__ d, int mo
   const PackDesc e = d[blockIdx.y];
   const size_t n = (size_t)e.Cout * e.Cin * e.NT;
   for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x)
-    e.out[j] = e.dgrad == 2 ? pack_slot_wino(e.w, e.Cout, e.Cin, mode, j) : pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
+    e.out[j] = e.dgrad == 2   ? pack_slot_wino(e.w, e.Cout, e.Cin, mode, j)
+               : e.dgrad == 3 ? pack_slot16(e.w, e.Cout, e.Cin, e.NT, mode, j)
+                              : pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
 }
 
 hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st) {

@@ -46,11 +46,13 @@ namespace sdp {
 
 constexpr int WPSTRIDE = 144;   // bytes per V pixel: 32 ch x (hi, lo) bf16 + 16 pad (conflict-free A reads)
 
-// acc += a * b on v_mfma_f32_16x16x32_bf16 with the accumulator tied in place ("+a"): with all 256
+// acc += a * b on v_mfma_f32_32x32x16_bf16 with the accumulator tied in place ("+a"): with all 256
 // AGPRs holding accumulators, the builtin's register allocation rotates every chain through
-// temporaries and parks accumulators in VGPRs (hundreds of v_accvgpr moves per chunk)
-SDP_DEV void mfma16x3(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+// temporaries and parks accumulators in VGPRs (hundreds of v_accvgpr moves per chunk).  The
+// 32x32 shape leaves 24 of its 32 issue cycles to the vector ALU (the 16x16x32 shape 8 of 16):
+// room for the input transform between the MFMAs
+SDP_DEV void mfma32(f32x16& c, const bf16x8& a, const bf16x8& b) {
+  asm("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
 template <int WM>
@@ -66,8 +68,8 @@ struct WinoTile {
   static constexpr int NITEM = PR * NP * 8;                  // (row, pair, 4-channel group) items
   static constexpr int NI = (NITEM + 255) / 256;             // items per thread (the last partial)
   static constexpr int WN = 4 / WM;                          // waves along N
-  static constexpr int MF = 4 / WM;                          // 16-pair M fragments per wave
   static constexpr int WROWS = TR / WM;                      // output rows per wave
+  static constexpr int MF = WROWS / 4;                       // 32-pair (4-row) M fragments per wave
   static constexpr int NTILE = WN * 64;                      // output channels per workgroup
   static constexpr int UOFF_BYTES = NU * 256 * 4;             // per-thread DMA offsets (kept out of VGPRs)
   static constexpr int LDS_BYTES = 2 * V_BYTES + 2 * RAW_BYTES + UOFF_BYTES;
@@ -108,40 +110,42 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
 
   const int Cin = a.Cin, Cout = a.Cout;
   const int nchunks = Cin / 32;
-  const int NF16 = Cout / 16;
+  const int NB32 = Cout / 32;
 
-  f32x4 acc[4][T::MF][4];                           // [position j][M fragment][16-Cout fragment]
+  f32x16 acc[4][T::MF][2];                          // [position j][M fragment][32-Cout fragment]
   static_for<0, 4>([&](auto j) {
     static_for<0, T::MF>([&](auto f) {
-      static_for<0, 4>([&](auto n) {
+      static_for<0, 2>([&](auto n) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[j][f][n][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[j][f][n][r] = 0.f;
       });
     });
   });
 
-  // ---- weights: [chunk][tap 12][16-Cout fragment][lane][hi 16 B | lo 16 B]; lane offset in a
-  // VGPR, the (chunk, tap) offset in an SGPR
+  // ---- weights: [chunk][tap 12][32-Cout fragment][q = (s0 hi, s0 lo, s1 hi, s1 lo)][lane][16 B]
+  // (train_aux.hip pack_slot_wino: every fragment load of a wave is 1 KiB contiguous); lane offset
+  // in a VGPR, the (chunk, tap) offset in an SGPR
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wfw, 0, 0x7fffffff, 0x00020000);
-  int wvo[4];
-  static_for<0, 4>([&](auto nc) {
-    constexpr int nj = decltype(nc)::value;
-    wvo[nj] = ((n0 / 16 + wn * 4 + nj) * 64 + lane) * 32;
+  int wvo[2];
+  static_for<0, 2>([&](auto nc) {
+    constexpr int nb = decltype(nc)::value;
+    wvo[nb] = ((n0 / 32 + wn * 2 + nb) * 256 + lane) * 16;
   });
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-  uint4 bq[3][4][2];                                // ring of 3 taps: [slot][nj][hi/lo]
+  uint4 bq[3][2][4];                                // ring of 3 taps: [slot][nb][(s, hi/lo)]
   auto load_b = [&](auto slot_c, int chunk, int tap) __attribute__((always_inline)) {
     constexpr int J = decltype(slot_c)::value;
     if constexpr (SDP_WKO & 4) return;
-    const int so = __builtin_amdgcn_readfirstlane((chunk * 12 + tap) * NF16 * 2048);
-    static_for<0, 4>([&](auto nc) {
-      constexpr int nj = decltype(nc)::value;
-      const u32x4 h = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvo[nj], so, 0);
-      bq[J][nj][0] = make_uint4(h.x, h.y, h.z, h.w);
-      if constexpr (X3) {
-        const u32x4 l = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvo[nj] + 16, so, 0);
-        bq[J][nj][1] = make_uint4(l.x, l.y, l.z, l.w);
-      }
+    const int so = __builtin_amdgcn_readfirstlane((chunk * 12 + tap) * NB32 * 4096);
+    static_for<0, 2>([&](auto nc) {
+      constexpr int nb = decltype(nc)::value;
+      static_for<0, 4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if constexpr (X3 || (q & 1) == 0) {
+          const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wrs, wvo[nb] + q * 1024, so, 0);
+          bq[J][nb][q] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+      });
     });
   };
 
@@ -256,14 +260,15 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
   __builtin_amdgcn_s_waitcnt(0xc07f);               // lgkmcnt(0)
   __syncthreads();
 
-  // A fragment (tap (kh, j), fragment f): lane l = pair m = l % 16 of the fragment, channels 8 (l / 16)
-  // .. ; fragment f covers wave rows 2f, 2f + 1 (m / 8) -> V pixel (j, wrow0 + 2f + m/8 + kh, m % 8)
-  const int a_lane = (wrow0 * T::NP + (lane & 15)) * WPSTRIDE + (lane >> 4) * 16;
+  // A fragment (tap (kh, j), fragment f, k step s): lane l = pair m = l % 32 of the fragment,
+  // channels 16 s + 8 (l / 32) .. ; fragment f covers wave rows 4f .. 4f + 3 (m / 8)
+  // -> V pixel (j, wrow0 + 4f + m/8 + kh, m % 8)
+  const int a_lane = (wrow0 * T::NP + (lane & 31)) * WPSTRIDE + (lane >> 5) * 16;
   auto read_a = [&](const char* vb, auto g_c, bf16x8& hi, bf16x8& lo) __attribute__((always_inline)) {
-    constexpr int g = decltype(g_c)::value;         // fragment sequence number: tap * MF + f
-    constexpr int tap = g / T::MF, f = g % T::MF, kh = tap / 4, j = tap % 4;
+    constexpr int g = decltype(g_c)::value;         // fragment sequence number: (tap * MF + f) * 2 + s
+    constexpr int s = g % 2, tap = g / 2 / T::MF, f = (g / 2) % T::MF, kh = tap / 4, j = tap % 4;
     if constexpr (SDP_WKO & 32) return;
-    const char* src = vb + ((j * T::PR + 2 * f + kh) * T::NP) * WPSTRIDE + a_lane;
+    const char* src = vb + ((j * T::PR + 4 * f + kh) * T::NP) * WPSTRIDE + a_lane + s * 32;
     hi = *reinterpret_cast<const bf16x8*>(src);
     if constexpr (X3) lo = *reinterpret_cast<const bf16x8*>(src + 64);
   };
@@ -321,26 +326,26 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
       constexpr bool XF = K < T::NI && !(SDP_WKO & 2);
       constexpr int NPC = PH == 0 ? 0 : (PH == 3 ? 8 : 4);   // pieces on this tap
       if constexpr (XF && PH == 0) item_load(std::integral_constant<int, K>{}, 1 - P, dv);
-      // blocks (f, pass): the 4 N fragments of fragment f, one operand pass each (fp32x3: lo*hi,
-      // hi*lo, hi*hi), so consecutive MFMAs feed 4 different accumulators
+      // blocks (f, s, pass): the 2 N fragments of fragment f at k step s, one operand pass each
+      // (fp32x3: lo*hi, hi*lo, hi*hi), so consecutive MFMAs feed different accumulators
       constexpr int NPASS = X3 ? 3 : 1;
-      constexpr int NBLK = T::MF * NPASS;
+      constexpr int NBLK = T::MF * 2 * NPASS;
       static_for<0, NBLK>([&](auto blk_c) {
         constexpr int blk = decltype(blk_c)::value;
-        constexpr int f = blk / NPASS, pass = blk % NPASS;
-        constexpr int g = tap * T::MF + f, AS = g % 3;
-        if constexpr (pass == 0 && g + 2 < 12 * T::MF)   // two fragments ahead
+        constexpr int fs = blk / NPASS, pass = blk % NPASS, f = fs / 2, sk = fs % 2;
+        constexpr int g = (tap * T::MF + f) * 2 + sk, AS = g % 3;
+        if constexpr (pass == 0 && g + 2 < 24 * T::MF)   // two fragments ahead
           read_a(vb, std::integral_constant<int, g + 2>{}, ahi[(g + 2) % 3], alo[(g + 2) % 3]);
-        static_for<0, 4>([&](auto njc) {
-          constexpr int nj = decltype(njc)::value;
-          const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&bq[CUR][nj][0]);
+        static_for<0, 2>([&](auto nbc) {
+          constexpr int nb = decltype(nbc)::value;
+          const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&bq[CUR][nb][2 * sk]);
           if constexpr (X3 && pass == 0) {
-            mfma16x3(acc[tap % 4][f][nj], alo[AS], bhi);
+            mfma32(acc[tap % 4][f][nb], alo[AS], bhi);
           } else if constexpr (X3 && pass == 1) {
-            const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&bq[CUR][nj][1]);
-            mfma16x3(acc[tap % 4][f][nj], ahi[AS], blo);
+            const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&bq[CUR][nb][2 * sk + 1]);
+            mfma32(acc[tap % 4][f][nb], ahi[AS], blo);
           } else {
-            mfma16x3(acc[tap % 4][f][nj], ahi[AS], bhi);
+            mfma32(acc[tap % 4][f][nb], ahi[AS], bhi);
           }
         });
         // piece i of this tap after block floor(i * NBLK / NPC)
@@ -387,46 +392,49 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
   }
 #endif
   if constexpr (SDP_WKO & 16) {   // knock-out: one store per lane keeps the accumulators live
-    float s = 0.f;
-    static_for<0, 4>([&](auto j) {
+    float sm = 0.f;
+    static_for<0, 4>([&](auto jj) {
       static_for<0, T::MF>([&](auto f) {
-        static_for<0, 4>([&](auto n) { s += acc[j][f][n][0] + acc[j][f][n][3]; });
+        static_for<0, 2>([&](auto n) { sm += acc[jj][f][n][0] + acc[jj][f][n][15]; });
       });
     });
-    a.out[(size_t)blockIdx.x * 256 + tid] = s;
+    a.out[(size_t)blockIdx.x * 256 + tid] = sm;
     return;
   }
   // ------------------------------------------------------------------ epilogue
-  // Register r of fragment (j, f, nj) of lane l: pair m = 4 (l / 16) + r of fragment f, i.e. wave
-  // row 2f + (l >> 5), pair 4 ((l >> 4) & 1) + r, Cout 16 nj + l % 16.  The lane holds output
-  // columns 8 ((l >> 4) & 1) .. +7 of that row: value i = 8 f + 2 r + e.
+  // Register r of fragment (j, f, nb) of lane l: pair m = (r & 3) + 8 (r >> 2) + 4 (l >> 5) of the
+  // fragment, i.e. wave row 4f + (r >> 2), pair (r & 3) + 4 (l >> 5), Cout 32 nb + l % 32.  Per
+  // (f, row rr = r >> 2) the lane holds output columns 8 (l >> 5) .. +7: value i = 32 f + 8 rr + 2 (r & 3) + e,
+  // and every wave store instruction writes 32 consecutive channels (128 B) of 2 pixels.
   {
     const int Wo = a.W;
     const size_t bo = (size_t)b * a.H * Wo * Cout;
     const int img_bytes = a.H * Wo * Cout * 4;
     auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p ? p + bo : a.out + bo), 0, img_bytes, 0x00020000); };
     const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), o2rs = rs(a.out2), r2rs = rs(a.res2);
-    const int lcol = lane & 15, lrow = lane >> 5, lhalf = (lane >> 4) & 1;
-    constexpr int NV = T::MF * 8;
+    const int lcol = lane & 31, lhalf = lane >> 5;
+    constexpr int NR = T::MF * 4;                     // output rows per lane
+    constexpr int NV = NR * 8;
     const int xs = d * Cout * 4;                     // bytes between consecutive output pixels of a run
-    static_for<0, 4>([&](auto njc) {
-      constexpr int nj = decltype(njc)::value;
-      const int co = n0 + wn * 64 + nj * 16 + lcol;
+    static_for<0, 2>([&](auto nbc) {
+      constexpr int nb = decltype(nbc)::value;
+      const int co = n0 + wn * 64 + nb * 32 + lcol;
       const float bias = a.bias ? a.bias[co] : 0.f;
-      int vbase[T::MF];
-      static_for<0, T::MF>([&](auto fc) {
-        constexpr int f = decltype(fc)::value;
-        const int y = (sr0 + wrow0 + 2 * f + lrow) * d + ph_r, x = (sc0 + 8 * lhalf) * d + ph_c;
-        vbase[f] = ((y * Wo + x) * Cout + co) * 4;
+      int vbase[NR];
+      static_for<0, NR>([&](auto rc) {
+        constexpr int rw = decltype(rc)::value;      // = 4 f + rr
+        const int y = (sr0 + wrow0 + rw) * d + ph_r, x = (sc0 + 8 * lhalf) * d + ph_c;
+        vbase[rw] = ((y * Wo + x) * Cout + co) * 4;
       });
       float v[NV];
       static_for<0, T::MF>([&](auto fc) {
         constexpr int f = decltype(fc)::value;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float m0 = acc[0][f][nj][r], m1 = acc[1][f][nj][r], m2 = acc[2][f][nj][r], m3 = acc[3][f][nj][r];
-          v[f * 8 + 2 * r] = ((m0 + m1) + m2) + bias;
-          v[f * 8 + 2 * r + 1] = ((m1 - m2) - m3) + bias;
+        for (int r = 0; r < 16; ++r) {
+          const float m0 = acc[0][f][nb][r], m1 = acc[1][f][nb][r], m2 = acc[2][f][nb][r], m3 = acc[3][f][nb][r];
+          const int i = f * 32 + (r >> 2) * 8 + (r & 3) * 2;
+          v[i] = ((m0 + m1) + m2) + bias;
+          v[i + 1] = ((m1 - m2) - m3) + bias;
         }
       });
       if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor
@@ -435,8 +443,8 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
         const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co;
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-          const int f = i / 8, k = i % 8;
-          const int y = (sr0 + wrow0 + 2 * f + lrow) * d + ph_r, x = (sc0 + 8 * lhalf + k) * d + ph_c;
+          const int rw = i / 8, k = i % 8;
+          const int y = (sr0 + wrow0 + rw) * d + ph_r, x = (sc0 + 8 * lhalf + k) * d + ph_c;
           const float fy = shh * (float)y, fx = sww * (float)x;
           const int y0 = (int)fy, x0 = (int)fx;
           const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
@@ -467,8 +475,8 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
       for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_WEPI_OFF(i), 2);
 #undef SDP_WEPI_OFF
       if (a.stats) {
-        // two-pass (mean, M2) over the lane's NV values, Chan merges of equal-count partials over the
-        // lanes of the same Cout: l ^ 16, then l ^ 32 -> the wave's 8/WM rows x 16 columns
+        // two-pass (mean, M2) over the lane's NV values, a Chan merge of equal-count partials with
+        // lane l ^ 32 (the other 8 columns) -> the wave's WROWS x 16 pixels of channel co
         float sum = 0.f;
 #pragma unroll
         for (int i = 0; i < NV; ++i) sum += v[i];
@@ -479,28 +487,23 @@ __global__ __launch_bounds__(256, 1) void wino_conv_kernel(ConvArgs a) {
           const float dv = v[i] - mean;
           m2 = fmaf(dv, dv, m2);
         }
-        float mp = __shfl_xor(mean, 16), qp = __shfl_xor(m2, 16), dm = mean - mp;
+        const float mp = __shfl_xor(mean, 32), qp = __shfl_xor(m2, 32), dm = mean - mp;
         m2 = m2 + qp + dm * dm * (0.5f * NV);
         mean = 0.5f * (mean + mp);
-        mp = __shfl_xor(mean, 32);
-        qp = __shfl_xor(m2, 32);
-        dm = mean - mp;
-        m2 = m2 + qp + dm * dm * (float)NV;
-        mean = 0.5f * (mean + mp);
         if constexpr (WM == 1) {
-          if (lane < 16) {
+          if (lane < 32) {
             float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile) * Cout + co;
             *st = make_float2(mean, m2);
           }
         } else {
           // the 128-pixel group is the whole tile: the two row waves merge through LDS (free now)
-          float2* xch = reinterpret_cast<float2*>(lds) + (wn * 4 + nj) * 16;
-          if (wm == 1 && lane < 16) xch[lane] = make_float2(mean, m2);
+          float2* xch = reinterpret_cast<float2*>(lds) + (wn * 2 + nb) * 32;
+          if (wm == 1 && lane < 32) xch[lane] = make_float2(mean, m2);
           __syncthreads();
-          if (wm == 0 && lane < 16) {
+          if (wm == 0 && lane < 32) {
             const float2 o = xch[lane];
             const float dd = mean - o.x;
-            m2 = m2 + o.y + dd * dd * (2.0f * NV);
+            m2 = m2 + o.y + dd * dd * (float)NV;
             mean = 0.5f * (mean + o.x);
             float2* st = reinterpret_cast<float2*>(a.stats) + ((size_t)b * a.groups_per_img + tile) * Cout + co;
             *st = make_float2(mean, m2);
