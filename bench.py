@@ -258,7 +258,21 @@ def run_sampling(args, rank, N, dist, dev):
             if args.mode == "viewsplit":
                 torch.distributed.all_gather_into_tensor(x_all, x)     # cross-view consistency gather
             torch.distributed.all_reduce(absmax, op=torch.distributed.ReduceOp.MAX)
-        merger(x_all, sig[c], setting, 10, 0.01, absmax)
+        if merge_ev is not None:
+            ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ea.record()
+            merger(x_all, sig[c], setting, 10, 0.01, absmax)
+            eb.record()
+            merge_ev.append((ea, eb))
+        else:
+            merger(x_all, sig[c], setting, 10, 0.01, absmax)
+
+    # consistency merge (9 kernels on the forward's stream), SURVEY §8(d) compulsory bytes per
+    # megabatch-step: per source view read x + mask + exist/sky, per output view write x and its
+    # 114 x W accumulator grid written and read (24 B per cell) -- 7.3 MB per view at N = 1
+    HWp = H * W
+    merge_bytes = n_src * (8 * HWp + 8 * HWp + 2 * HWp) + V * (8 * HWp + 2 * 24 * ((50 * H) // 28) * W)
+    merge_ev = None
 
     def measure(prec, steps, warmup):
         """Time `steps` steps with the score net at conv arithmetic `prec` (profiling OFF), then a
@@ -274,11 +288,15 @@ def run_sampling(args, rank, N, dist, dev):
         psteps = min(steps, 5)
         cur.profile(True)
         cur.profile_read()
+        nonlocal merge_ev
+        merge_ev = []
         for i in range(psteps):
             step(warmup + steps + i)
         torch.cuda.synchronize()
         prof = cur.profile_read()
         cur.profile(False)
+        merge_us = sum(ea.elapsed_time(eb) for ea, eb in merge_ev) / len(merge_ev) * 1e3
+        merge_ev = None
         steps = psteps                                  # per-step figures below are over the profiled pass
         if rank == 0:
             for k, (n_, ms_, fl_, by_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
@@ -299,6 +317,11 @@ def run_sampling(args, rank, N, dist, dev):
                 mem.append({"kernel": k, "launches_per_step": round(n_ / steps, 2), "avg_launch_us": round(t_ * 1e6, 2),
                             "algorithmic_bytes": int(by_), "achieved_GBps": round(by_ / t_ / 1e9, 1),
                             "frac": round(by_ / t_ / 1e9 / HBM_PEAK, 4)})
+        mem.append({"kernel": "consistency_merge (9 kernels, HIP events around sdp_consistency_merge)",
+                    "launches_per_step": 1, "avg_launch_us": round(merge_us, 2), "algorithmic_bytes": int(merge_bytes),
+                    "achieved_GBps": round(merge_bytes / (merge_us * 1e-6) / 1e9, 1),
+                    "frac": round(merge_bytes / (merge_us * 1e-6) / 1e9 / HBM_PEAK, 4),
+                    "bytes_basis": "SURVEY 8(d): 7.3 MB per view; latency/atomic-bound, not HBM-bound"})
         traffic, tsrc = pmc_traffic(prec, V, cls) if args.workload == "line" else (None, None)
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[prec], 1),
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK[prec], 4),

@@ -148,6 +148,18 @@ class Runner:
             return tuple(b)
         return fetch
 
+    def _active_group(self, n_mega, world):
+        """The process group of the ranks that hold megabatches (they share tooHigh), created once
+        per active set and reused by later sample() calls (every rank joins new_group); None on one
+        process.  Ranks without megabatches idle through the sampling calls."""
+        if world <= 1:
+            return None
+        active = tuple(r for r in range(world) if shard_megabatches(n_mega, r, world)[1] > shard_megabatches(n_mega, r, world)[0])
+        cache = self.__dict__.setdefault("_groups", {})
+        if active not in cache:
+            cache[active] = torch.distributed.group.WORLD if len(active) == world else torch.distributed.new_group(list(active))
+        return cache[active]
+
     def _gather(self, t, world):
         """Rank-ordered concatenation of every rank's [n, ...] CPU tensor (None = no views)."""
         if world == 1:
@@ -173,16 +185,13 @@ class Runner:
         ex = torch.from_numpy(np.broadcast_to(synthetic.exist_mask(H, W), (B, H, W)).copy())
         folder = self.args.image_folder
         ck = c.sampling.ckpt_id
-        n_batches = getattr(self.args, "num_batches", 1)
+        n_batches = getattr(self.args, "num_batches", None) or 1
         time_taken = np.zeros(aB)
         end_point, to_add = aB, 0
         if ds == "KITTI360_im_simultaneous_densification":   # AllForOne:553-558
             end_point, to_add = 2, aB - 2
         m0, m1 = shard_megabatches(n_mega, rank, world)
-        group = None
-        if world > 1:   # the ranks that hold megabatches share tooHigh (every rank joins new_group)
-            active = [r for r in range(world) if shard_megabatches(n_mega, r, world)[1] > shard_megabatches(n_mega, r, world)[0]]
-            group = torch.distributed.new_group(active)
+        group = self._active_group(n_mega, world)
         writer = rank == 0
         fetch = self._batch_source(ds, B, aB, H, W)
         for bi in range(n_batches):
@@ -311,15 +320,12 @@ class Runner:
         folder = self.args.image_folder
         ck = c.sampling.ckpt_id
         fetch, n_val = self._completion_source(B, aB, H, W)
-        n_batches = min(getattr(self.args, "num_batches", 1) or n_val, n_val)
+        n_batches = min(getattr(self.args, "num_batches", None) or 1, n_val)
         time_taken = np.zeros(max(n_val, 2)) + 999999
         writer = rank == 0
-        group = torch.distributed.group.WORLD if world > 1 else None
         n_mega = B // aB
         m0, m1 = shard_megabatches(n_mega, rank, world)
-        if world > 1 and not all(shard_megabatches(n_mega, r, world)[1] > shard_megabatches(n_mega, r, world)[0]
-                                 for r in range(world)):
-            raise ValueError(f"scene completion: {n_mega} megabatches cannot feed {world} ranks")
+        group = self._active_group(n_mega, world)     # ranks without megabatches idle, as in sample()
         for bi in range(n_batches):
             ref_full, mask_full, sky_full, idx_full, names, origins = fetch(bi)
             save_num = names[0]
@@ -339,13 +345,15 @@ class Runner:
                 sl = slice(m0 * aB, m1 * aB)
                 self._sync()
                 t0 = time.time()
-                outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic(
-                    init[sl], ref[sl], mask[sl], sky_full[sl], None, 2, 7, score, sigmas, mods, aB,
-                    c.sampling.n_steps_each, c.sampling.step_lr, existMask=ex[sl], denoise=c.sampling.denoise,
-                    grad_ref=1, correlation_coefficient=0.01, sampling_step=4, dist_group=group,
-                    noise_views=(sl.start, B), ops=self.ops)
-                final = self._gather(outs[-1], world)
-                shared = self._gather(outs[-2], world)
+                outs = None
+                if m1 > m0:
+                    outs, _, _ = anneal_Langevin_dynamics_inpainting_simultaneous_basic(
+                        init[sl], ref[sl], mask[sl], sky_full[sl], None, 2, 7, score, sigmas, mods, aB,
+                        c.sampling.n_steps_each, c.sampling.step_lr, existMask=ex[sl], denoise=c.sampling.denoise,
+                        grad_ref=1, correlation_coefficient=0.01, sampling_step=4, dist_group=group,
+                        noise_views=(sl.start, B), ops=self.ops)
+                final = self._gather(None if outs is None else outs[-1], world)
+                shared = self._gather(None if outs is None else outs[-2], world)
                 self._sync()
                 time_taken[do] += time.time() - t0
                 if not writer:
@@ -394,6 +402,59 @@ class Runner:
             b = kitti360.collate([dset[j] for j in items[rank * Bt:(rank + 1) * Bt]])
             return b[0], b[1], b[2]
         return fetch
+
+    def _test_source(self, Bt):
+        """Test batches of the every-100-steps EMA evaluation (kitti:84-95, 247-251): the test split
+        of the dataset (``get_dataset``'s second return) through its own MySampler iterator, never
+        the training iterator.  Only rank 0 evaluates, so the draws (the sampler shuffles and every
+        item's roll come from the global np.random stream) run on a saved-and-restored np.random
+        state: the ranks' training streams stay in lockstep and their global-batch slices disjoint."""
+        c = self.config
+        H, W = c.data.image_size, c.data.image_width
+        root = getattr(self.args, "kitti_root", None)
+        if not root:
+            seed = getattr(self.args, "seed", 1234)
+
+            def synth(i):
+                sc = synthetic.scene_views(Bt, H, W, seed=seed + 7919 * i + 1)
+                ref, mask = torch.from_numpy(sc["ref"]), torch.from_numpy(sc["mask"])
+                return ref * mask, mask, torch.from_numpy(sc["sky"])
+            return synth
+        dset = kitti360.get_dataset(c.data.dataset, None, c, split="test", root=root, device=self.device)
+        n_batches = max(1, len(dset) // Bt)
+        state = {"it": None}
+
+        def fetch(i):
+            saved = np.random.get_state()
+            try:
+                items = []
+                for _ in range(Bt):
+                    try:
+                        if state["it"] is None:
+                            raise StopIteration
+                        items.append(next(state["it"]))
+                    except StopIteration:    # the reference re-creates test_iter on exhaustion
+                        state["it"] = iter(kitti360.MySampler(n_batches, Bt, random=True))
+                        items.append(next(state["it"]))
+                b = kitti360.collate([dset[j] for j in items])
+            finally:
+                np.random.set_state(saved)
+            return b[0], b[1], b[2]
+        return fetch
+
+    def _batches_per_epoch(self, Bt, world):
+        """One epoch = one pass of the DataLoader over the training split (kitti:172): the dataset's
+        len // (Bt * world) global batches with --kitti_root; --num_batches overrides it (and is the
+        epoch length of the procedural source, which has no length)."""
+        nb = getattr(self.args, "num_batches", None)
+        if nb:
+            return nb
+        root = getattr(self.args, "kitti_root", None)
+        if root:
+            c = self.config
+            dset = kitti360.get_dataset(c.data.dataset, None, c, split="train", root=root, device=self.device)
+            return max(1, len(dset) // (Bt * world))
+        return 1
 
     def _initial_state_dict(self):
         """Random-init weights; with --resume_training the reference's shape-filtered partial
@@ -490,9 +551,10 @@ class Runner:
         sig = torch.as_tensor(sigmas, dtype=torch.float32, device=self.device)
         Bt = c.training.batch_size
         source = self._train_source(Bt, rank, world)
+        test_source = self._test_source(Bt) if rank == 0 else None
         gen = torch.Generator(device=self.device).manual_seed(getattr(self.args, "seed", 1234) + rank)
         max_epochs = getattr(self.args, "max_epochs", None) or getattr(c.training, "n_epochs", 500000)
-        batches_per_epoch = getattr(self.args, "num_batches", None) or 1
+        batches_per_epoch = self._batches_per_epoch(Bt, world)
         step = true_step = 0
         max_t = 1
         self.losses = []
@@ -516,7 +578,7 @@ class Runner:
                     if step >= c.training.n_iters:
                         return 0
                     if step % 100 == 0 and t == 0 and rank == 0:
-                        tl = self._test_loss(trainer, source(10 ** 6 + step), sigmas, max_t, gen)
+                        tl = self._test_loss(trainer, test_source(step // 100), sigmas, max_t, gen)
                         logging.info("step: {}, test_loss: {}".format(step, tl))
                     if true_step % 20 == 0 and max_t < len(sigmas):
                         max_t += 1
