@@ -296,3 +296,36 @@ def sampler_kitti(x, ref, mask, sky, min_step, setting, allowance, score, sigmas
     x = (x + F32(grad_ref) * lik).astype(F32)
     images.append(x)
     return images, [], shared
+
+
+def sampler_allforone(x, ref, mask, sky, min_step, setting, score, sigmas, mods, aB, n_steps_each, step_lr, exist,
+                      noise_fn, denoise=True, grad_ref=1.0, cc=0.01):
+    """anneal_Langevin_dynamics_inpainting_simultaneous_basic (models/__init__.py:112-602): the cc
+    ramp of settings 5/6 (L209-212), per step score + nan_to_num + update (L236-259), from level
+    minStepToShare on the origin-offset merge (L263-519; its newImages kept at levels 0/20/110 and
+    the last, L505-508), denoise with the stale likelihood and the final data consistency (L580-599)."""
+    images, shared = [], []
+    lik = None
+    L = len(sigmas)
+    for c, sigma in enumerate(sigmas):
+        if setting == 5:
+            cc = 1 / (L / (c + 1))
+        if setting == 6:
+            cc = 0.5 / (L / (c + 1))
+        s = step_size_of(step_lr, sigma, sigmas[-1])
+        for _ in range(n_steps_each):
+            gr = nan_to_num(score(x, np.full(x.shape[0], c, np.int64)))
+            x, lik = langevin_update(x, gr, ref, mask, noise_fn(x.shape), s, grad_ref)
+            if c >= min_step:
+                new, x = allforone_merge(x, mask, sky, exist, mods, aB, sigma, setting, cc)
+                if c in (0, 20, 110):
+                    shared.append(new)
+                if c == L - 1:
+                    images.append(new)
+    if denoise:
+        gr = score(x, np.full(x.shape[0], L - 1, np.int64))
+        x = ((x + F32(sigmas[-1]) ** 2 * gr) + F32(grad_ref) * lik).astype(F32)
+    lik = (-mask).astype(F32) * (x - ref)
+    x = (x + F32(grad_ref) * lik).astype(F32)
+    images.append(x)
+    return images, [], shared

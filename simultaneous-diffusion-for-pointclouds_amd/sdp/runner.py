@@ -127,8 +127,17 @@ class Runner:
             net.load_state_dict(states[0], states[-1] if c.model.ema else None)
         else:
             logging.warning("checkpoint %s not found: using synthetic random-init weights", ckpt)
-            net.load_synthetic()
+            net.load_state_dict(self._synthetic_sd())
         return net
+
+    def _synthetic_sd(self):
+        """Synthetic weights with the model's sigma buffer of THIS config: NCSN registers
+        get_sigmas(config) (ncsnv2.py:430), and the score is divided by it (ncsnv2.py:516)."""
+        c = self.config
+        sd = synthetic_state_dict(c.model.ngf, c.data.channels, c.model.num_classes)
+        sd["sigmas"] = get_sigmas_np(c.model.sigma_begin, c.model.sigma_end, c.model.num_classes,
+                                     getattr(c.model, "sigma_dist", "geometric"))
+        return sd
 
     def _png(self, grid_views, name, nrow):
         """make_grid + save_image of a [2B',3,H,W] layout (kitti:658-661)."""
@@ -460,8 +469,7 @@ class Runner:
         """Random-init weights; with --resume_training the reference's shape-filtered partial
         load of a list-format checkpoint (kitti:115-128: keys whose shape matches replace the
         fresh weights, the rest stay random)."""
-        c = self.config
-        sd = synthetic_state_dict(c.model.ngf, c.data.channels, c.model.num_classes)
+        sd = self._synthetic_sd()
         if getattr(self.args, "resume_training", False):
             path = getattr(self.args, "ckpt", None) or "diffusionNet/checkpoint_148.pth"
             states = torch.load(path, map_location="cpu", weights_only=True)

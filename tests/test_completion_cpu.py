@@ -54,6 +54,9 @@ def test_completion_runner_files(tmp_path, monkeypatch):
         def load_synthetic(self):
             return self
 
+        def load_state_dict(self, sd, ema_shadow=None):
+            return self
+
     def a41(init, ref, mask, sky, idx, start, setting, score, sigmas, mods, aB, *a, **kw):
         log.append((init.shape[0], start, setting, tuple(mods.shape), kw["correlation_coefficient"], kw["grad_ref"]))
         return [init + 0.5, init * 2], [], []
