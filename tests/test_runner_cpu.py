@@ -20,6 +20,9 @@ class _FakeNet:
     def load_synthetic(self):
         return self
 
+    def load_state_dict(self, sd, ema_shadow=None):
+        return self
+
 
 def _config(name, B=14, W=128):
     with open(os.path.join(CFG_DIR, name)) as f:
