@@ -17,11 +17,24 @@
 
 namespace sdp {
 
+// 128-channel outputs on 2-wave workgroups (128 px x 128 Cout, two per CU) instead of 256 px x 128
+// Cout (one per CU): SDP_HALF=0 turns it off
+static int half_wg() {   // 0 = off, 1 = 128-channel outputs, 2 = also the 256-channel outputs
+  static const int h = [] {
+    const char* e = getenv("SDP_HALF");
+    return e ? atoi(e) : 1;
+  }();
+  return h;
+}
+
 template <int MODE, bool PELU>
-static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
+static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, bool half, hipStream_t st) {
   if (ks == 1) return conv_launch<MODE, 1, 64, 1, true, PELU>(a, st);   // only the ConvMeanPool 1x1 shortcut
   if (pool) return conv_launch<MODE, 1, 64, 3, true, PELU>(a, st);
   if constexpr (MODE != MODE_F32) {   // 16-wide tiles: the 16x16 MFMA shape only
+#ifndef SDP_CONV_BENCH_ONLY
+    if (half) return conv_launch_half<MODE, PELU>(a, st);
+#endif
     if (tc == 16) return wm == 2 ? conv_launch<MODE, 2, 16, 3, false, PELU>(a, st) : conv_launch<MODE, 1, 16, 3, false, PELU>(a, st);
   }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, PELU>(a, st);
@@ -29,13 +42,13 @@ static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int t
 }
 
 template <int MODE>
-static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st) {
+static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st, bool half = false) {
 #ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, true>(a, st);
   return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, true>(a, st) : conv_launch<MODE, 1, 32, 3, false, true>(a, st);
 #else
-  return a.pro_mode == PRO_NONE ? launch_elu<MODE, false>(a, ks, pool, wm, tc, st)
-                                : launch_elu<MODE, true>(a, ks, pool, wm, tc, st);
+  return a.pro_mode == PRO_NONE ? launch_elu<MODE, false>(a, ks, pool, wm, tc, half, st)
+                                : launch_elu<MODE, true>(a, ks, pool, wm, tc, half, st);
 #endif
 }
 
@@ -106,10 +119,13 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (mode == MODE_F32) return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
   return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
 #endif
+  // 128-channel outputs: 2-wave workgroups of 8 x 16 pixels (16x16 shape, 3x3 non-pooled)
+  const bool half = (wm == 2 ? half_wg() >= 1 : half_wg() >= 2) && sh16 && ks == 3 && !pool && Ws % 16 == 0 &&
+                    Hs % 8 == 0;
   switch (mode) {
     case MODE_F32: return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
-    case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
-    default: return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st);
+    case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st, half);
+    default: return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st, half);
   }
 }
 

@@ -1,7 +1,8 @@
 // Definitions + explicit instantiations of the conv launchers (conv_launch.h).
 //
 // Built once per kernel shape (Makefile: conv_i_<code>.o with -DSDP_INST=<code>):
-//   forward : code = 100 * (mode + 1) + 10 * pelu + shape   (shape = index into FwdShape)
+//   forward : code = 100 * (mode + 1) + 10 * pelu + shape   (shape = index into FwdShape; 7 = the
+//             2-wave workgroups of conv_launch_half)
 //   dgrad   : code = 1000 + 10 * mode + shape                (shape = index into DgradShape)
 // Without SDP_INST (tools/conv_bench, -DSDP_CONV_BENCH_ONLY) it instantiates the 3x3 non-pooled
 // ELU-prologue forward shapes of every mode, which is all that bench dispatches.
@@ -50,6 +51,16 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   return hipErrorInvalidValue;   // (not reached: conv.hip picks 16-wide tiles for the 16x16 forward only)
 }
 
+template <int MODE, bool PELU>
+hipError_t conv_launch_half(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<1, 16, 3, 2>;
+  a.tiles_per_img = a.H * a.W / (T::TR * 16);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, 2>), grid, dim3(T::NTH), 0, st, a);
+  return hipGetLastError();
+}
+
 template <int MODE, int WM, int TC, int KS, bool ZP>
 hipError_t dgrad_launch(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS>;
@@ -79,7 +90,11 @@ template <> struct DgradShape<2> { static constexpr int WM = 2, TC = 32, KS = 3;
 template <> struct DgradShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool ZP = false; };
 template <> struct DgradShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool ZP = false; };
 
-#if defined(SDP_INST) && SDP_INST < 1000
+#if defined(SDP_INST) && SDP_INST < 1000 && SDP_INST % 10 == 7
+constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10;
+static_assert(kMode >= 1 && kMode <= 2 && kPelu <= 1, "SDP_INST: bad 2-wave forward code");
+template hipError_t conv_launch_half<kMode, (kPelu != 0)>(ConvArgs, hipStream_t);
+#elif defined(SDP_INST) && SDP_INST < 1000
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
 static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && kShape <= 6 && (kShape < 5 || kMode != MODE_F32),
               "SDP_INST: bad forward code");

@@ -60,9 +60,12 @@ namespace sdp {
 
 constexpr int PSTRIDE = 144;  // bytes per staged patch pixel: 32 ch x (hi,lo bf16) or 32 x f32, + 16 pad
 
-template <int WM, int TC, int KS>
+// NW = waves per workgroup: 4 (one workgroup per CU), or 2 (128-pixel x 128-Cout workgroups, two
+// per CU: one's prologue and epilogue run under the other's MFMAs)
+template <int WM, int TC, int KS, int NW = 4>
 struct ConvTile {
-  static constexpr int WN = 4 / WM;                // waves along N
+  static constexpr int NTH = 64 * NW;              // threads per workgroup
+  static constexpr int WN = NW / WM;               // waves along N
   static constexpr int RW = 128 / TC;              // pixel rows per wave
   static constexpr int TR = WM * RW;               // tile rows
   static constexpr int NTILE = WN * 64;            // output channels per workgroup
@@ -70,14 +73,14 @@ struct ConvTile {
   static constexpr int PC = TC + 2 * HALO;
   static constexpr int PR = TR + 2 * HALO;
   static constexpr int NPIX = PR * PC;
-  static constexpr int NU = (NPIX * 8 + 255) / 256;            // 16-B staging units per thread per chunk
-  static constexpr int PATCH_BYTES = NU * 32 * PSTRIDE;         // one transformed patch (+ slack: every
+  static constexpr int NU = (NPIX * 8 + NTH - 1) / NTH;        // 16-B staging units per thread per chunk
+  static constexpr int PATCH_BYTES = NU * (NTH / 8) * PSTRIDE;  // one transformed patch (+ slack: every
                                                                 //   staging unit has a pixel slot)
-  static constexpr int RAW_BYTES = NU * 256 * 16;               // raw fp32 patch landed by LDS-DMA
+  static constexpr int RAW_BYTES = NU * NTH * 16;               // raw fp32 patch landed by LDS-DMA
   static constexpr int PIPE_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
   static constexpr int EPI_BYTES = WM * 64 * (NTILE + 8) * 4;   // LDS-staged epilogue (one half)
   static constexpr int LDS_BYTES = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(LDS_BYTES * (4 / NW) <= 160 * 1024, "LDS budget (4 / NW workgroups per CU)");
 };
 
 SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -89,11 +92,13 @@ SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p);
 // give-back' item 7).  SH = 16 is forward-only (direct epilogue, no dact) and reads the SAME packed
 // weights: a lane fetches the (cout, 8-channel group) its 16x16 fragment needs from the 32x32
 // packing by its own buffer offset.
-template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32>
-__global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
+template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
   static_assert(SH == 32 || (SH == 16 && MODE != MODE_F32), "16x16 shape: bf16 modes only");
-  using T = ConvTile<WM, TC, KS>;
+  static_assert(NW == 4 || (SH == 16 && !POOL), "2-wave workgroups: the 16x16 non-pooled forward only");
+  using T = ConvTile<WM, TC, KS, NW>;
+  constexpr int NTH = T::NTH;
   constexpr int NT = KS * KS;
   constexpr int NU = T::NU;
   constexpr int XT = NT >= 4 ? 4 : NT;            // taps that carry the transform of the next chunk
@@ -225,7 +230,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   unsigned uvalid = 0;
   static_for<0, NU>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    int u = tid + k * 256;
+    int u = tid + k * NTH;
     bool valid = u < T::NPIX * 8;
     u = valid ? u : 0;
     const int pix = u >> 3, cv = u & 7;
@@ -247,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   auto load_unit = [&](auto kc, int chunk) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     if constexpr (SDP_KO & 1) return;
-    const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * 256) * 16);
+    const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * NTH) * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
         uoff[k], chunk * 128, 0, SDP_DMA_AUX);
@@ -256,12 +261,12 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
   auto xform_load = [&](auto kc) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
-    return *reinterpret_cast<const float4*>(raw + (tid + k * 256) * 16);
+    return *reinterpret_cast<const float4*>(raw + (tid + k * NTH) * 16);
   };
   auto xform_store = [&](auto kc, auto pb, float4 v) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     constexpr int PB = decltype(pb)::value;
-    const int pix = (tid + k * 256) >> 3;   // units past the patch land in its slack: no branch
+    const int pix = (tid + k * NTH) >> 3;   // units past the patch land in its slack: no branch
     v.x = fmaf(v.x, ssv0.x, ssv0.y);
     v.y = fmaf(v.y, ssv0.z, ssv0.w);
     v.z = fmaf(v.z, ssv1.x, ssv1.y);
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
   auto xform_piece = [&](auto kc, auto hc, auto pb, float4 v4) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value, h = decltype(hc)::value, PB = decltype(pb)::value;
     if constexpr (SDP_KO & 2) return;
-    const int pix = (tid + k * 256) >> 3;
+    const int pix = (tid + k * NTH) >> 3;
     float x0 = h ? v4.z : v4.x, x1 = h ? v4.w : v4.y;
     const float4 sv = h ? ssv1 : ssv0;
     x0 = fmaf(x0, sv.x, sv.y);
@@ -618,7 +623,7 @@ __global__ __launch_bounds__(256, 1) void conv_mfma_kernel(ConvArgs a) {
       }
     });
   } else if (a.dact) {
-    if constexpr (TC >= 32) {   // (TC = 16 tiles are forward-only, 16x16 shape)
+    if constexpr (TC >= 32 && NW == 4) {   // (TC = 16 tiles and 2-wave workgroups are forward-only, 16x16 shape)
     // data-gradient launches (training): the LDS-staged epilogue -- its 16-B pixel-row
     // accesses of the elu' operand and the residual gradient beat per-channel 4-B accesses
     // ------------------------------------------------------------------ epilogue

@@ -11,6 +11,11 @@ namespace sdp {
 template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
 hipError_t conv_launch(ConvArgs a, hipStream_t st);
 
+// forward conv of the 128-channel layers on 2-wave workgroups (128 px x 128 Cout, two per CU),
+// bf16 modes on the 16x16 shape (conv_inst.hip shape 7)
+template <int MODE, bool PELU>
+hipError_t conv_launch_half(ConvArgs a, hipStream_t st);
+
 // data gradient (conv_bwd.hip dispatch)
 template <int MODE, int WM, int TC, int KS, bool ZP>
 hipError_t dgrad_launch(ConvArgs a, hipStream_t st);
