@@ -146,12 +146,12 @@ def cpu_baseline_train(H, W, threads):
                       f"(torch CPU fp32), {dt:.2f} s"}
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
 
 
 def pmc_traffic(precision, V, cls):
     """HBM bytes per launch of the dominant conv class, read from the committed PMC passes
-    (tools/pmc_traffic.sh -> profiles/r02_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
+    (tools/class_traffic.sh -> profiles/r03_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
     correction) + TCC_EA0_WRREQ bytes per launch of that kernel at this grid).  PMC counters cannot
     be read inside this process, so the value is tagged with the hash of the conv kernel's sources
     (sdp/_build.py conv_source_hash: common.h, conv_kernel.h, conv.hip -- what tools/conv_bench is

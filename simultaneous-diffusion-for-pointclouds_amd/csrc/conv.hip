@@ -44,6 +44,9 @@ static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int t
 template <int MODE>
 static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st, bool half = false) {
 #ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
+  if constexpr (MODE != MODE_F32) {
+    if (half) return conv_launch_half<MODE, true>(a, st);
+  }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, true>(a, st);
   return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, true>(a, st) : conv_launch<MODE, 1, 32, 3, false, true>(a, st);
 #else
@@ -56,6 +59,7 @@ static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int 
 // whose sub-grid tiles into 8 x 16 pixels.  SDP_WINO (bit mask, default 3): 1 = 256-channel outputs
 // (128 px x 256 Cout workgroups), 2 = 128-channel outputs (128 px x 128 Cout); 0 = direct only
 // (default while the Winograd kernel is slower than the direct one).
+#ifndef SDP_CONV_BENCH_ONLY
 static int wino_mask() {
   static const int m = [] {
     const char* e = getenv("SDP_WINO");
@@ -69,16 +73,19 @@ static hipError_t wino_mode(const ConvArgs& a, int wm, hipStream_t st) {
   if (wm == 1) return a.pro_mode == PRO_NONE ? wino_launch<MODE, 1, false>(a, st) : wino_launch<MODE, 1, true>(a, st);
   return a.pro_mode == PRO_NONE ? wino_launch<MODE, 2, false>(a, st) : wino_launch<MODE, 2, true>(a, st);
 }
+#endif
 
 // Host entry: validates the shape contract the kernel's indexing assumes, then launches.
 hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, const char** why) {
   const int d = a.dil;
+#ifndef SDP_CONV_BENCH_ONLY   // (tools/conv_bench times the direct kernel; tools/wino_bench the Winograd one)
   if (a.wfw && mode != MODE_F32 && ks == 3 && !pool && a.circular && !a.dact && a.Cin % 64 == 0 && a.H % d == 0 &&
       a.W % d == 0 && (a.H / d) % 8 == 0 && (a.W / d) % 16 == 0 && a.pro_ss &&
       (a.Cin <= 1024 || a.ss_bstride != 0)) {
     const int wm = a.Cout % 256 == 0 ? 1 : (a.Cout % 128 == 0 ? 2 : 0);
     if (wm && (wino_mask() & wm)) return mode == MODE_F32X3 ? wino_mode<MODE_F32X3>(a, wm, st) : wino_mode<MODE_BF16>(a, wm, st);
   }
+#endif
   if (a.Cin % 64 || a.Cout % 128) { *why = "conv: Cin%64 and Cout%128 required"; return hipErrorInvalidValue; }
   if (a.H % d || a.W % d) { *why = "conv: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
   const int Hs = a.H / d, Ws = a.W / d;
@@ -114,14 +121,14 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (!a.circular && d != 1) { *why = "conv: zero padding only for d=1"; return hipErrorInvalidValue; }
   if (!a.pro_ss) { *why = "conv: prologue scale/shift table missing"; return hipErrorInvalidValue; }
   if (a.Cin > 1024 && a.ss_bstride == 0) { *why = "conv: identity table holds 1024 channels"; return hipErrorInvalidValue; }
-#ifdef SDP_CONV_BENCH_ONLY
-  if (mode == MODE_BF16) return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st);
-  if (mode == MODE_F32) return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
-  return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st);
-#endif
   // 128-channel outputs: 2-wave workgroups of 8 x 16 pixels (16x16 shape, 3x3 non-pooled)
   const bool half = (wm == 2 ? half_wg() >= 1 : half_wg() >= 2) && sh16 && ks == 3 && !pool && Ws % 16 == 0 &&
                     Hs % 8 == 0;
+#ifdef SDP_CONV_BENCH_ONLY
+  if (mode == MODE_BF16) return launch_mode<MODE_BF16>(a, ks, pool, wm, tc, st, half);
+  if (mode == MODE_F32) return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
+  return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st, half);
+#endif
   switch (mode) {
     case MODE_F32: return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
     case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st, half);

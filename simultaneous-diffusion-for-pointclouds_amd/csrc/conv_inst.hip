@@ -114,6 +114,8 @@ template hipError_t dgrad_launch<kMode, DS::WM, DS::TC, DS::KS, DS::ZP>(ConvArgs
 SDP_BENCH_INST(MODE_F32)
 SDP_BENCH_INST(MODE_F32X3)
 SDP_BENCH_INST(MODE_BF16)
+template hipError_t conv_launch_half<MODE_F32X3, true>(ConvArgs, hipStream_t);
+template hipError_t conv_launch_half<MODE_BF16, true>(ConvArgs, hipStream_t);
 #undef SDP_BENCH_INST
 #else
 #error "conv_inst.hip: build with -DSDP_INST=<code> (Makefile) or -DSDP_CONV_BENCH_ONLY (tools/conv_bench)"
