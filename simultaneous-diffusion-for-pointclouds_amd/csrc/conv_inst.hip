@@ -37,6 +37,7 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS>;
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
+  a.strip_w = conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / TC);
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   if constexpr (MODE != MODE_F32) {
     if (!a.dact && mfma_shape() == 16) {
@@ -56,6 +57,8 @@ hipError_t conv_launch_half(ConvArgs a, hipStream_t st) {
   using T = ConvTile<1, 16, 3, 2>;
   a.tiles_per_img = a.H * a.W / (T::TR * 16);
   a.groups_per_img = a.H * a.W / 128;
+  a.strip_w = 0;   // row-major: strips cut this class's reads 229 -> 177 MB but cost 2.6 % of time
+                   // (profiles/experiments/r03_strip_ab.log)
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, 2>), grid, dim3(T::NTH), 0, st, a);
   return hipGetLastError();

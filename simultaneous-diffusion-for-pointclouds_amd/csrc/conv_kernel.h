@@ -124,7 +124,17 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   const int ph = t / tiles_rc;
   t -= ph * tiles_rc;
   const int ph_r = ph / d, ph_c = ph - (ph / d) * d;
-  const int sr0 = (t / tiles_c) * T::TR, sc0 = (t % tiles_c) * TC;
+  int trow, tcol;
+  if (a.strip_w) {   // strips of strip_w tile columns x all tile rows (common.h conv_strip_w)
+    const int R = Hs / T::TR, sw = a.strip_w;
+    const int strip = t / (R * sw), w_ = t - strip * (R * sw);
+    trow = w_ / sw;
+    tcol = strip * sw + (w_ - trow * sw);
+  } else {
+    trow = t / tiles_c;
+    tcol = t % tiles_c;
+  }
+  const int sr0 = trow * T::TR, sc0 = tcol * TC;
   const int n0 = blockIdx.y * T::NTILE;
   const int wrow0 = wm * T::RW;                    // wave's first tile row
 
