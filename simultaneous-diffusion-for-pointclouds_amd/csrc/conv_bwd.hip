@@ -18,10 +18,23 @@
 
 namespace sdp {
 
+// 8 x 16 pixel tiles (the forward's: a 10 x 18 patch, 1.41x the pixels, against 4 x 66 = 2.06x for
+// the 2 x 64 tiles) with the direct 16x16 epilogue -- the 128-channel outputs on 2-wave workgroups.
+// Opt-in (SDP_DGRAD16=1): the bf16 training step runs 60.5 -> 64.3 ms with it (the direct epilogue's
+// per-element elu' and residual loads; profiles/experiments/r03_dgrad16_train_ab.log)
+static bool dgrad16() {
+  static const bool on = [] {
+    const char* e = getenv("SDP_DGRAD16");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return on;
+}
+
 template <int MODE>
-static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, hipStream_t st) {
+static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, bool t16, hipStream_t st) {
   if (ks == 1) return dgrad_launch<MODE, 2, 32, 1, false>(a, st);
   if (!a.circular) return dgrad_launch<MODE, 2, 32, 3, true>(a, st);
+  if (t16) return wm == 2 ? dgrad_launch_half<MODE>(a, st) : dgrad_launch<MODE, 1, 16, 3, false>(a, st);
   if (wm == 2) return dgrad_launch<MODE, 2, 32, 3, false>(a, st);
   return tc == 64 ? dgrad_launch<MODE, 1, 64, 3, false>(a, st) : dgrad_launch<MODE, 1, 32, 3, false>(a, st);
 }
@@ -45,9 +58,12 @@ hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char**
   if (a.dact && !a.aux) { *why = "dgrad: dact needs aux"; return hipErrorInvalidValue; }
   if (a.dact == 3 && !a.epi_ss) { *why = "dgrad: dact 3 needs epi_ss"; return hipErrorInvalidValue; }
   if (!a.pro_ss) { *why = "dgrad: prologue identity table missing"; return hipErrorInvalidValue; }
+  // 16-wide tiles: the 16x16 MFMA shape (the default; SDP_DGRAD_SHAPE=32 keeps the 32x32 one)
+  const char* shp = getenv("SDP_DGRAD_SHAPE");
+  const bool t16 = dgrad16() && !(shp && atoi(shp) == 32) && ks == 3 && a.circular && Ws % 16 == 0 && Hs % 8 == 0;
   switch (mode) {
-    case MODE_F32X3: return launch_dgrad_mode<MODE_F32X3>(a, ks, wm, tc, st);
-    case MODE_BF16: return launch_dgrad_mode<MODE_BF16>(a, ks, wm, tc, st);
+    case MODE_F32X3: return launch_dgrad_mode<MODE_F32X3>(a, ks, wm, tc, t16, st);
+    case MODE_BF16: return launch_dgrad_mode<MODE_BF16>(a, ks, wm, tc, t16, st);
     default: *why = "dgrad: training runs in fp32x3 or bf16"; return hipErrorInvalidValue;
   }
 }

@@ -70,10 +70,11 @@ hipError_t dgrad_launch(ConvArgs a, hipStream_t st) {
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  if (dgrad_shape() == 16)
+  if (TC < 32 || dgrad_shape() == 16) {
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
-  else
+  } else if constexpr (TC >= 32) {
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -86,12 +87,23 @@ template <> struct FwdShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; s
 template <> struct FwdShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool POOL = false; };
 template <> struct FwdShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
 template <> struct FwdShape<6> { static constexpr int WM = 2, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
+template <int MODE>
+hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<1, 16, 3, 2>;
+  a.tiles_per_img = a.H * a.W / (T::TR * 16);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, false, 16, 2>), grid, dim3(T::NTH), 0, st, a);
+  return hipGetLastError();
+}
+
 template <int S> struct DgradShape;
 template <> struct DgradShape<0> { static constexpr int WM = 2, TC = 32, KS = 1; static constexpr bool ZP = false; };
 template <> struct DgradShape<1> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool ZP = true; };
 template <> struct DgradShape<2> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool ZP = false; };
 template <> struct DgradShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool ZP = false; };
 template <> struct DgradShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool ZP = false; };
+template <> struct DgradShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool ZP = false; };  // 16x16 shape only
 
 #if defined(SDP_INST) && SDP_INST < 1000 && SDP_INST % 10 == 7
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10;
@@ -103,9 +115,13 @@ static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && kShape <= 6 && (kShape <
               "SDP_INST: bad forward code");
 using FS = FwdShape<kShape>;
 template hipError_t conv_launch<kMode, FS::WM, FS::TC, FS::KS, FS::POOL, (kPelu != 0)>(ConvArgs, hipStream_t);
+#elif defined(SDP_INST) && SDP_INST % 10 == 6
+constexpr int kMode = (SDP_INST / 10) % 10;
+static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16), "SDP_INST: bad dgrad code");
+template hipError_t dgrad_launch_half<kMode>(ConvArgs, hipStream_t);
 #elif defined(SDP_INST)
 constexpr int kMode = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
-static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16) && kShape <= 4,
+static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16) && kShape <= 5,
               "SDP_INST: bad dgrad code");
 using DS = DgradShape<kShape>;
 template hipError_t dgrad_launch<kMode, DS::WM, DS::TC, DS::KS, DS::ZP>(ConvArgs, hipStream_t);

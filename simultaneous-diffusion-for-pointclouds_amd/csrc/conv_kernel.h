@@ -515,7 +515,9 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   }
 
   SDP_T(3);
-  if (SH == 16 && !a.dact) {
+  // the direct 16x16 epilogue: every forward, and the data-gradient launches of the 16-wide tiles
+  // and 2-wave workgroups (the LDS-staged epilogue below needs TC >= 32 and 4 waves)
+  if (SH == 16 && (!a.dact || TC < 32 || NW != 4)) {
     // ------------------------------------------------------------------ epilogue, 16x16 fragments
     // Register r of fragment (mb, nj) of lane l holds pixel 4 (l / 16) + r of the fragment's 16-px
     // row segment and Cout 16 nj + l % 16 of the wave's 64: every wave store writes four 64-B runs
@@ -526,7 +528,7 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
     const size_t bo = (size_t)b * Ho * Wo * Cout;
     const int img_bytes = Ho * Wo * Cout * 4;
     auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p ? p + bo : a.out + bo), 0, img_bytes, 0x00020000); };
-    const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), o2rs = rs(a.out2), r2rs = rs(a.res2);
+    const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), o2rs = rs(a.out2), r2rs = rs(a.res2), xrs = rs(a.aux);
     const int lq = lane >> 4, lcol = lane & 15;
     constexpr int CB = TC / 16;                      // 16-px fragments per tile row
     constexpr int NF = POOL ? CB : 8;                // fragments (pooled: row-0 fragments) per lane
@@ -586,6 +588,19 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
         }
       }
 #define SDP_EPI16_OFF(i) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs)
+      if (a.dact) {   // backward: * the derivative of the ELU that followed this tensor (ConvArgs::dact)
+        float esc = 1.f, esh = 0.f;
+        if (a.dact == 3) {
+          esc = a.epi_ss[((size_t)b * Cout + co) * 2];
+          esh = a.epi_ss[((size_t)b * Cout + co) * 2 + 1];
+        }
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI16_OFF(i), 0));
+          if (a.dact == 3) h = fmaf(h, esc, esh);
+          v[i] = v[i] * elu_grad(h, a.dact);
+        }
+      }
       if (a.res) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, SDP_EPI16_OFF(i), 0)) + v[i];

@@ -16,6 +16,10 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st);
 template <int MODE, bool PELU>
 hipError_t conv_launch_half(ConvArgs a, hipStream_t st);
 
+// data gradient of the 128-channel layers on 2-wave workgroups (conv_inst.hip dgrad shape 6)
+template <int MODE>
+hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st);
+
 // data gradient (conv_bwd.hip dispatch)
 template <int MODE, int WM, int TC, int KS, bool ZP>
 hipError_t dgrad_launch(ConvArgs a, hipStream_t st);
