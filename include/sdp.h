@@ -20,6 +20,7 @@
  *   sdp_dsm_loss           anneal_dsm_score_estimation_with_mask            losses/dsm.py:67-119
  *   sdp_net_backward       loss.backward()                                  runners/ncsn_runner_kitti_simultaneous.py:230
  *   sdp_adam_ema_step      optimizer.step() (Adam, losses/__init__.py:10-20) + EMAHelper.update (models/ema.py:16-21)
+ *   sdp_optim_ema_step     optimizer.step() of Adam / RMSprop / SGD (get_optimizer, losses/__init__.py:3-13) + EMA
  *   sdp_range_project      point_cloud_to_range_image                       datasets/lidar_utils.py:54-347
  *   sdp_view_transform     pose chain fromWorld @ (toWorld @ p)             datasets/kitti360_im_8Batch.py:146-190
  *   sdp_view_gather        scanPoints[index[index >= 0]]                    datasets/kitti360_im_simultenous_densification.py:186-203
@@ -136,6 +137,17 @@ int sdp_dsm_loss(const float* score, const float* noise, const float* mask, cons
 int sdp_adam_ema_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema_shadow,
                       size_t n, float lr, float beta1, float beta2, float eps, int step, float ema_mu,
                       void* stream);
+/* optimizer.step() of every optimizer get_optimizer builds (losses/__init__.py:3-13), in torch's
+ * per-element order, then the EMA update as above.  g <- g + weight_decay*p first (all kinds).
+ *   SDP_OPTIM_ADAM    state0 exp_avg, state1 exp_avg_sq, state2 max_exp_avg_sq (amsgrad) or NULL;
+ *                     betas (beta1, beta2)
+ *   SDP_OPTIM_RMSPROP state0 square_avg; beta2 = alpha (torch default 0.99), eps (default 1e-8)
+ *   SDP_OPTIM_SGD     state0 momentum_buffer (written as g on step 1); beta1 = momentum, dampening 0
+ * step = 1, 2, ... (the optimizer's step count after this step).                            */
+enum sdp_optim_kind { SDP_OPTIM_ADAM = 0, SDP_OPTIM_RMSPROP = 1, SDP_OPTIM_SGD = 2 };
+int sdp_optim_ema_step(int kind, float* params, const float* grads, float* state0, float* state1, float* state2,
+                       float* ema_shadow, size_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
+                       int step, float ema_mu, void* stream);
 
 /* ---- Langevin update ------------------------------------------------------------------ *
  * x <- x + step*g' + grad_ref*lik + noise*noise_scale   (float32, reference evaluation order)

@@ -49,8 +49,19 @@ hipError_t end_conv_backward(const float* dscore, const float* sigmas, const int
                              int W, hipStream_t st);
 hipError_t dsm_loss(const float* score, const float* noise, const float* mask, const float* used_sigma, int B, int n_img,
                     float power, float* dscore, float* loss, float* loss_per, float* part, hipStream_t st);
-hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow, size_t n, float b1, float b2, float eps,
-                    float step_size, float bc2_sqrt, float mu, hipStream_t st);
+// optimizer kinds of get_optimizer (losses/__init__.py:3-13); values = sdp.h SDP_OPTIM_*
+enum { OPT_ADAM = 0, OPT_RMSPROP = 1, OPT_SGD = 2 };
+struct OptimHyper {
+  float b1, b2;          // Adam betas; RMSprop: b2 = alpha; SGD: b1 = momentum
+  float eps, weight_decay;
+  float step_size;       // Adam: lr / bias_correction1; RMSprop, SGD: lr
+  float bc2_sqrt;        // Adam: sqrt(bias_correction2)
+  float mu;              // EMA rate
+  int first;             // SGD: first step (momentum buffer = g)
+};
+// s0, s1, s2: Adam exp_avg, exp_avg_sq, max_exp_avg_sq (amsgrad, else null); RMSprop square_avg; SGD momentum_buffer
+hipError_t optim_ema(int kind, float* p, const float* g, float* s0, float* s1, float* s2, float* shadow, size_t n,
+                     const OptimHyper& h, hipStream_t st);
 hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char** why);
 // weight-gradient workgroups per launch (pixel splits x Cin/32 x Cout/128): one round of
 // two workgroups per CU (1024: +2% kernel time and a costlier reduce)

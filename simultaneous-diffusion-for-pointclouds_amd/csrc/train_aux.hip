@@ -787,31 +787,58 @@ hipError_t dsm_loss(const float* score, const float* noise, const float* mask, c
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- Adam + EMA
-// torch.optim.Adam (weight_decay 0, amsgrad off):
-//   m = m + (1-b1)(g - m) ; v = b2 v + (1-b2) g^2 ; p -= step_size * m / (sqrt(v)/bc2_sqrt + eps)
-// EMAHelper.update: shadow = (1-mu) p + mu shadow
-__global__ void adam_ema_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                                float* __restrict__ v, float* __restrict__ shadow, size_t n, float b1, float b2,
-                                float eps, float step_size, float bc2_sqrt, float mu) {
+// ---------------------------------------------------------------- optimizer step + EMA
+// get_optimizer (losses/__init__.py:3-13) -- the torch.optim update of every optimizer it builds, in
+// torch's per-element evaluation order, then EMAHelper.update (ema.py:16-21):
+//   Adam    : g += wd p ; m = m + (1-b1)(g - m) ; v = b2 v + (1-b2) g^2 ; [amsgrad: vmax = max(vmax, v)]
+//             p -= step_size * m / (sqrt(v or vmax)/bc2_sqrt + eps)
+//   RMSprop : g += wd p ; v = alpha v + (1-alpha) g^2 ; p -= lr * g / (sqrt(v) + eps)
+//   SGD     : g += wd p ; buf = first step ? g : momentum buf + (1-dampening) g ; p -= lr * buf
+//   EMA     : shadow = (1-mu) p + mu shadow
+template <int KIND>
+__global__ void optim_ema_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ s0,
+                                 float* __restrict__ s1, float* __restrict__ s2, float* __restrict__ shadow, size_t n,
+                                 OptimHyper h) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const float gi = g[i];
-    float mi = m[i];
-    mi = mi + (1.f - b1) * (gi - mi);
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    const float pi = p[i] - step_size * (mi / denom);
+    float pi = p[i];
+    float gi = g[i];
+    if (h.weight_decay != 0.f) gi = gi + h.weight_decay * pi;   // torch._foreach_add(grads, params, alpha=wd)
+    if constexpr (KIND == OPT_ADAM) {
+      float mi = s0[i];
+      mi = mi + (1.f - h.b1) * (gi - mi);                        // lerp(m, g, 1-b1), weight < 0.5 branch
+      const float vi = s1[i] * h.b2 + (1.f - h.b2) * gi * gi;
+      s0[i] = mi;
+      s1[i] = vi;
+      float vd = vi;
+      if (s2) {                                                   // amsgrad: max_exp_avg_sq
+        vd = fmaxf(s2[i], vi);
+        s2[i] = vd;
+      }
+      const float denom = sqrtf(vd) / h.bc2_sqrt + h.eps;
+      pi = pi - h.step_size * (mi / denom);
+    } else if constexpr (KIND == OPT_RMSPROP) {
+      const float vi = s0[i] * h.b2 + (1.f - h.b2) * gi * gi;   // b2 = alpha
+      s0[i] = vi;
+      pi = pi - h.step_size * (gi / (sqrtf(vi) + h.eps));
+    } else {                                                      // SGD with momentum b1, dampening 0
+      const float bi = h.first ? gi : s0[i] * h.b1 + gi;
+      s0[i] = bi;
+      pi = pi - h.step_size * bi;
+    }
     p[i] = pi;
-    if (shadow) shadow[i] = (1.f - mu) * pi + mu * shadow[i];
+    if (shadow) shadow[i] = (1.f - h.mu) * pi + h.mu * shadow[i];
   }
 }
 
-hipError_t adam_ema(float* p, const float* g, float* m, float* v, float* shadow, size_t n, float b1, float b2, float eps,
-                    float step_size, float bc2_sqrt, float mu, hipStream_t st) {
-  hipLaunchKernelGGL(adam_ema_kernel, dim3(grid_for(n)), dim3(256), 0, st, p, g, m, v, shadow, n, b1, b2, eps, step_size,
-                     bc2_sqrt, mu);
+hipError_t optim_ema(int kind, float* p, const float* g, float* s0, float* s1, float* s2, float* shadow, size_t n,
+                     const OptimHyper& h, hipStream_t st) {
+  const dim3 grid(grid_for(n)), block(256);
+  switch (kind) {
+    case OPT_ADAM: hipLaunchKernelGGL(optim_ema_kernel<OPT_ADAM>, grid, block, 0, st, p, g, s0, s1, s2, shadow, n, h); break;
+    case OPT_RMSPROP: hipLaunchKernelGGL(optim_ema_kernel<OPT_RMSPROP>, grid, block, 0, st, p, g, s0, s1, s2, shadow, n, h); break;
+    case OPT_SGD: hipLaunchKernelGGL(optim_ema_kernel<OPT_SGD>, grid, block, 0, st, p, g, s0, s1, s2, shadow, n, h); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

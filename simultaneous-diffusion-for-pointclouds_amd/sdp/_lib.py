@@ -62,6 +62,7 @@ _SIGS = {
     "sdp_net_backward": (I, [P, P, I, P, SZ, P, P]),
     "sdp_dsm_loss": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
     "sdp_adam_ema_step": (I, [P, P, P, P, P, SZ, F, F, F, F, I, F, P]),
+    "sdp_optim_ema_step": (I, [I, P, P, P, P, P, P, SZ, F, F, F, F, F, I, F, P]),
     "sdp_range_project_workspace_size": (I, [I, I, C.POINTER(SZ)]),
     "sdp_range_project": (I, [P, I, I, I, P, I, I, P, P, P, P, P, P, SZ, P]),
     "sdp_view_transform": (I, [P, C.c_int64, P, P, P, P]),

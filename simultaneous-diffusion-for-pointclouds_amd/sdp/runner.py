@@ -489,13 +489,7 @@ class Runner:
         that ``ScoreNet.load_checkpoint`` / the sampler's loader read back."""
         sd = {"module." + k: v.cpu() for k, v in trainer.state_dict().items()}
         sd["module.sigmas"] = trainer.net.sigmas.clone()
-        ids = {k: i for i, (k, _, _) in enumerate(trainer.layout)}
-        state = {ids[k]: {"step": torch.tensor(float(trainer.steps)), "exp_avg": a.cpu(), "exp_avg_sq": q.cpu()}
-                 for (k, a), (_, q) in zip(trainer.named_parameters(trainer.exp_avg),
-                                           trainer.named_parameters(trainer.exp_avg_sq))}
-        optim = {"state": state, "param_groups": [{"lr": trainer.lr, "betas": (trainer.beta1, trainer.beta2),
-                                                   "eps": trainer.eps, "weight_decay": 0.0, "amsgrad": False,
-                                                   "params": list(range(len(trainer.layout)))}]}
+        optim = trainer.optimizer_state_dict()
         states = [sd, optim, epoch, step]
         if trainer.shadow is not None:
             states.append({k: v.cpu() for k, v in trainer.ema_state_dict().items()})

@@ -6,9 +6,10 @@ Mirrors the reference's training interface:
     ``sdp_dsm_loss``;
   * ``Trainer.backward()`` -- ``loss.backward()`` (runners/ncsn_runner_kitti_simultaneous.py:230)
     through ``sdp_net_backward``;
-  * ``Trainer.step()`` -- ``optimizer.step()`` of ``get_optimizer`` (losses/__init__.py:10-20,
-    Adam) and ``EMAHelper.update`` (models/ema.py:16-21) in one fused kernel, then the packed
-    conv weights are rebuilt on the device;
+  * ``Trainer.step()`` -- ``optimizer.step()`` of ``get_optimizer`` (losses/__init__.py:3-13:
+    Adam with weight_decay / amsgrad, RMSprop, SGD with momentum 0.9) and ``EMAHelper.update``
+    (models/ema.py:16-21) in one fused kernel, then the packed conv weights are rebuilt on the
+    device;
   * ``train_step`` -- one inner-loop iteration of the kitti runner's ``train()``
     (runners/ncsn_runner_kitti_simultaneous.py:186-235).
 
@@ -26,15 +27,27 @@ from .scorenet import ScoreNet
 
 class Trainer:
     """Device-resident training state of one ScoreNet: parameter arena (bound to the net),
-    gradient arena, Adam moments and the EMA shadow, all in the net's parameter layout."""
+    gradient arena, optimizer state and the EMA shadow, all in the net's parameter layout.
+
+    ``optimizer``: "Adam" (betas (beta1, beta2), eps, weight_decay, amsgrad), "RMSProp"
+    (torch.optim.RMSprop: alpha 0.99, eps 1e-8, weight_decay) or "SGD" (momentum 0.9) --
+    the three optimizers of get_optimizer (losses/__init__.py:3-13)."""
+
+    OPTIMIZERS = {"Adam": 0, "RMSProp": 1, "SGD": 2}
 
     def __init__(self, net: ScoreNet, lr: float = 1e-4, beta1: float = 0.9, beta2: float = 0.999,
-                 eps: float = 1e-8, ema: bool = True, ema_mu: float = 0.999, device="cuda", dist_group=None):
+                 eps: float = 1e-8, ema: bool = True, ema_mu: float = 0.999, device="cuda", dist_group=None,
+                 optimizer: str = "Adam", weight_decay: float = 0.0, amsgrad: bool = False,
+                 alpha: float = 0.99, momentum: float = 0.9):
         if net.precision not in ("fp32x3", "bf16"):
             raise ValueError("training runs in precision fp32x3 or bf16")
+        if optimizer not in self.OPTIMIZERS:
+            raise NotImplementedError("Optimizer {} not understood.".format(optimizer))   # losses/__init__.py:12-13
         L = _lib.lib()
         self.net, self.L = net, L
+        self.optimizer = optimizer
         self.lr, self.beta1, self.beta2, self.eps = lr, beta1, beta2, eps
+        self.weight_decay, self.amsgrad, self.alpha, self.momentum = float(weight_decay), bool(amsgrad), alpha, momentum
         self.ema, self.ema_mu = ema, ema_mu
         self.dist_group = dist_group
         n = _lib.SZ()
@@ -51,8 +64,12 @@ class Trainer:
         self.params = torch.empty(n.value, dtype=torch.float32, device=device)
         _lib.check(L.sdp_net_bind_params(net._h, self.params.data_ptr(), _lib.stream()), "bind_params")
         self.grads = torch.zeros_like(self.params)
-        self.exp_avg = torch.zeros_like(self.params)
-        self.exp_avg_sq = torch.zeros_like(self.params)
+        # optimizer state buffers (torch's state names)
+        names = {"Adam": ["exp_avg", "exp_avg_sq"] + (["max_exp_avg_sq"] if self.amsgrad else []),
+                 "RMSProp": ["square_avg"], "SGD": ["momentum_buffer"]}[optimizer]
+        self.opt_state = {k: torch.zeros_like(self.params) for k in names}
+        self.exp_avg = self.opt_state.get("exp_avg")
+        self.exp_avg_sq = self.opt_state.get("exp_avg_sq")
         self.shadow = self.params.clone() if ema else None       # EMAHelper.register (ema.py:10-14)
         self.steps = 0
         self._ws = {}
@@ -136,14 +153,39 @@ class Trainer:
             self.grads.div_(dist.get_world_size(self.dist_group))
 
     def step(self):
-        """optimizer.step() (Adam) + ema_helper.update(score), then re-pack the conv weights."""
+        """optimizer.step() + ema_helper.update(score), then re-pack the conv weights."""
         self.steps += 1
-        _lib.check(self.L.sdp_adam_ema_step(self.params.data_ptr(), self.grads.data_ptr(), self.exp_avg.data_ptr(),
-                                            self.exp_avg_sq.data_ptr(),
-                                            self.shadow.data_ptr() if self.shadow is not None else None,
-                                            self.params.numel(), self.lr, self.beta1, self.beta2, self.eps,
-                                            self.steps, self.ema_mu, _lib.stream()), "adam_ema_step")
+        st = list(self.opt_state.values()) + [None, None]
+        kind = self.OPTIMIZERS[self.optimizer]
+        if kind == 0:
+            b1, b2, eps = self.beta1, self.beta2, self.eps
+        elif kind == 1:
+            b1, b2, eps = 0.0, self.alpha, 1e-8          # torch.optim.RMSprop defaults (alpha, eps)
+        else:
+            b1, b2, eps = self.momentum, 0.0, 0.0
+        ptr = lambda t: t.data_ptr() if t is not None else None
+        _lib.check(self.L.sdp_optim_ema_step(kind, self.params.data_ptr(), self.grads.data_ptr(), ptr(st[0]),
+                                             ptr(st[1]), ptr(st[2]), ptr(self.shadow), self.params.numel(),
+                                             self.lr, b1, b2, eps, self.weight_decay, self.steps, self.ema_mu,
+                                             _lib.stream()), "optim_ema_step")
         _lib.check(self.L.sdp_net_repack(self.net._h, _lib.stream()), "repack")
+
+    def optimizer_state_dict(self):
+        """optimizer.state_dict() in torch's format (per-parameter state keyed by index)."""
+        state = {}
+        for i, (k, off, numel) in enumerate(self.layout):
+            e = {n: t[off:off + numel].view(self.shapes[k]).cpu() for n, t in self.opt_state.items()}
+            if self.optimizer != "SGD":
+                e["step"] = torch.tensor(float(self.steps))
+            state[i] = e
+        group = {"lr": self.lr, "weight_decay": self.weight_decay, "params": list(range(len(self.layout)))}
+        if self.optimizer == "Adam":
+            group.update(betas=(self.beta1, self.beta2), eps=self.eps, amsgrad=self.amsgrad)
+        elif self.optimizer == "RMSProp":
+            group.update(alpha=self.alpha, eps=1e-8, momentum=0, centered=False)
+        else:
+            group.update(momentum=self.momentum, dampening=0, nesterov=False)
+        return {"state": state, "param_groups": [group]}
 
 
 def anneal_dsm_score_estimation_with_mask(scorenet: Trainer, perturbed_samples, used_sigmas, noise, masks, sky,
@@ -175,15 +217,19 @@ def dsm_loss_value(scores, used_sigmas, noise, masks, anneal_power=2.0):
 
 
 def get_optimizer(config, net: ScoreNet, **kw) -> Trainer:
-    """losses/__init__.py:10-20 (Adam only: the shipped configs' optimizer)."""
+    """losses/__init__.py:3-13: Adam(lr, weight_decay, betas=(beta1, 0.999), amsgrad, eps),
+    RMSprop(lr, weight_decay), SGD(lr, momentum=0.9); anything else raises NotImplementedError."""
     o = config.optim
-    if o.optimizer != "Adam":
-        raise NotImplementedError(f"optimizer {o.optimizer}: only Adam is built")
-    if getattr(o, "weight_decay", 0.0) or getattr(o, "amsgrad", False):
-        raise NotImplementedError("Adam with weight_decay / amsgrad is not built")
     ema = bool(getattr(config.model, "ema", True))
-    return Trainer(net, lr=o.lr, beta1=o.beta1, beta2=0.999, eps=o.eps, ema=ema,
-                   ema_mu=getattr(config.model, "ema_rate", 0.999), **kw)
+    common = dict(ema=ema, ema_mu=getattr(config.model, "ema_rate", 0.999), **kw)
+    if o.optimizer == "Adam":
+        return Trainer(net, lr=o.lr, beta1=o.beta1, beta2=0.999, eps=o.eps, optimizer="Adam",
+                       weight_decay=getattr(o, "weight_decay", 0.0), amsgrad=getattr(o, "amsgrad", False), **common)
+    if o.optimizer == "RMSProp":
+        return Trainer(net, lr=o.lr, optimizer="RMSProp", weight_decay=getattr(o, "weight_decay", 0.0), **common)
+    if o.optimizer == "SGD":
+        return Trainer(net, lr=o.lr, optimizer="SGD", momentum=0.9, **common)
+    raise NotImplementedError("Optimizer {} not understood.".format(o.optimizer))
 
 
 def train_step(trainer: Trainer, X, originalX, mask, sigmas, timestep: int, step_lr: float, n_steps_each: int,

@@ -120,6 +120,58 @@ def test_adam_ema_step_matches_torch():
     assert torch.allclose(tr.shadow.cpu(), shadow, rtol=1e-6, atol=1e-7)
 
 
+@pytest.mark.parametrize("name", ["Adam-wd-amsgrad", "RMSProp", "RMSProp-wd", "SGD"])
+def test_get_optimizer_kinds_match_torch(name):
+    """Every optimizer of get_optimizer (losses/__init__.py:3-13) against torch.optim on the same
+    gradients, 3 steps, plus the EMA shadow; built through get_optimizer from a config namespace."""
+    from types import SimpleNamespace as NS
+    from sdp.training import get_optimizer
+    kind = name.split("-")[0]
+    wd = 1e-2 if ("wd" in name) else 0.0
+    ams = "amsgrad" in name
+    cfg = NS(optim=NS(optimizer=kind, lr=1e-3, weight_decay=wd, beta1=0.9, amsgrad=ams, eps=1e-8),
+             model=NS(ema=True, ema_rate=0.999))
+    net = ScoreNet(H=H, W=W, precision="fp32x3").load_synthetic()
+    tr = get_optimizer(cfg, net)
+    p0 = tr.params.cpu().clone()
+    ref_p = torch.nn.Parameter(p0.clone())
+    if kind == "Adam":      # losses/__init__.py:5-7
+        opt = torch.optim.Adam([ref_p], lr=1e-3, weight_decay=wd, betas=(0.9, 0.999), amsgrad=ams, eps=1e-8)
+    elif kind == "RMSProp":  # :9
+        opt = torch.optim.RMSprop([ref_p], lr=1e-3, weight_decay=wd)
+    else:                    # :11
+        opt = torch.optim.SGD([ref_p], lr=1e-3, momentum=0.9)
+    g = torch.Generator().manual_seed(1)
+    shadow = p0.clone()
+    for _ in range(3):
+        grad = torch.randn(p0.shape, generator=g)
+        tr.grads.copy_(grad.cuda())
+        tr.step()
+        ref_p.grad = grad
+        opt.step()
+        shadow = (1 - 0.999) * ref_p.data + 0.999 * shadow
+    torch.cuda.synchronize()
+    assert torch.allclose(tr.params.cpu(), ref_p.data, rtol=1e-6, atol=1e-7)
+    assert torch.allclose(tr.shadow.cpu(), shadow, rtol=1e-6, atol=1e-7)
+    # the state_dict in torch's format carries the same optimizer state
+    sd = tr.optimizer_state_dict()
+    ref_state = opt.state[ref_p]
+    for k, v in sd["state"][0].items():
+        if k == "step":
+            assert float(v) == float(ref_state["step"])
+        else:
+            n = v.numel()
+            assert torch.allclose(v.flatten(), ref_state[k].flatten()[:n], rtol=1e-5, atol=1e-7), k
+
+
+def test_get_optimizer_unknown_raises():
+    from types import SimpleNamespace as NS
+    from sdp.training import get_optimizer
+    net = ScoreNet(H=H, W=W, precision="fp32x3").load_synthetic()
+    with pytest.raises(NotImplementedError):
+        get_optimizer(NS(optim=NS(optimizer="Adagrad", lr=1e-3), model=NS()), net)
+
+
 def test_repacked_weights_follow_the_optimizer():
     """After step() the forward uses the updated parameters (device re-pack)."""
     net = ScoreNet(H=H, W=W, precision="fp32x3").load_synthetic()
