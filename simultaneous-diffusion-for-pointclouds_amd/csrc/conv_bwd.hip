@@ -19,13 +19,15 @@
 namespace sdp {
 
 // 8 x 16 pixel tiles (the forward's: a 10 x 18 patch, 1.41x the pixels, against 4 x 66 = 2.06x for
-// the 2 x 64 tiles) with the direct 16x16 epilogue -- the 128-channel outputs on 2-wave workgroups.
-// Opt-in (SDP_DGRAD16=1): the bf16 training step runs 60.5 -> 64.3 ms with it (the direct epilogue's
-// per-element elu' and residual loads; profiles/experiments/r03_dgrad16_train_ab.log)
+// the 2 x 64 tiles) with the transposed direct 16x16 epilogue (conv_kernel.h TRN: 16-B elu' operand,
+// residual and output accesses) -- the 128-channel outputs on 2-wave workgroups.  The default since
+// the transposed epilogue: bf16 training step 132.8 -> 137.0 image-steps/s (with 4-B accesses it was
+// 60.5 -> 64.3 ms slower; profiles/experiments/r03_dgrad16_train_ab.log, r03_trans_ab.log).
+// SDP_DGRAD16=0 keeps the 2 x 64 tiles with the LDS-staged epilogue.
 static bool dgrad16() {
   static const bool on = [] {
     const char* e = getenv("SDP_DGRAD16");
-    return e ? atoi(e) != 0 : false;
+    return e ? atoi(e) != 0 : true;
   }();
   return on;
 }

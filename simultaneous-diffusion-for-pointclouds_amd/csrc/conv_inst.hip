@@ -70,9 +70,11 @@ hipError_t dgrad_launch(ConvArgs a, hipStream_t st) {
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  if (TC < 32 || dgrad_shape() == 16) {
+  if constexpr (TC < 32) {   // 8 x 16 tiles: the transposed direct epilogue (conv_kernel.h TRN)
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16, 4, true>), grid, dim3(256), 0, st, a);
+  } else if (dgrad_shape() == 16) {
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
-  } else if constexpr (TC >= 32) {
+  } else {
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
   }
   return hipGetLastError();
@@ -93,7 +95,7 @@ hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st) {
   a.tiles_per_img = a.H * a.W / (T::TR * 16);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, false, 16, 2>), grid, dim3(T::NTH), 0, st, a);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, false, 16, 2, true>), grid, dim3(T::NTH), 0, st, a);
   return hipGetLastError();
 }
 

@@ -92,7 +92,14 @@ SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p);
 // give-back' item 7).  SH = 16 is forward-only (direct epilogue, no dact) and reads the SAME packed
 // weights: a lane fetches the (cout, 8-channel group) its 16x16 fragment needs from the 32x32
 // packing by its own buffer offset.
-template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4>
+// TRN (data-gradient launches on the 16x16 shape): the MFMAs compute D = W x X (weights as the A
+// operand, the patch as B -- the same fragment registers), so a lane's 4 accumulators are 4
+// consecutive output channels of ONE pixel and every epilogue load/store is 16 B per lane (32 per
+// wave and tensor instead of 128 of 4 B).  The forward keeps D = X x W: measured in the network,
+// D = W x X made the fp32x3 forward convs 2-3 % slower (256->256 165 -> 170 us, 128->128 @64x1024
+// 209 -> 213 us) while the bf16 training step ran 132.8 -> 137.0 image-steps/s with the transposed
+// direct epilogue on the data gradient (profiles/experiments/r03_trans_ab.log).
+template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4, bool TRN = false>
 __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
   static_assert(SH == 32 || (SH == 16 && MODE != MODE_F32), "16x16 shape: bf16 modes only");
@@ -100,6 +107,7 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   using T = ConvTile<WM, TC, KS, NW>;
   constexpr int NTH = T::NTH;
   constexpr int NT = KS * KS;
+  constexpr bool TRANS = TRN && SH == 16 && !POOL;
   constexpr int NU = T::NU;
   constexpr int XT = NT >= 4 ? 4 : NT;            // taps that carry the transform of the next chunk
   __shared__ __attribute__((aligned(16))) char lds[T::LDS_BYTES];
@@ -482,12 +490,21 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
             const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
             const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
             const bf16x8 ahi = s == 0 ? c0_hi[i] : c1_hi[i];
-            if constexpr (MODE == MODE_F32X3) {
-              const bf16x8 alo = s == 0 ? c0_lo[i] : c1_lo[i];
-              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc4[mb][nj], 0, 0, 0);
-              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc4[mb][nj], 0, 0, 0);
+            if constexpr (TRANS) {   // D = W x X: rows = Cout, columns = pixels (same fragment registers)
+              if constexpr (MODE == MODE_F32X3) {
+                const bf16x8 alo = s == 0 ? c0_lo[i] : c1_lo[i];
+                acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi, alo, acc4[mb][nj], 0, 0, 0);
+                acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blo, ahi, acc4[mb][nj], 0, 0, 0);
+              }
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi, ahi, acc4[mb][nj], 0, 0, 0);
+            } else {
+              if constexpr (MODE == MODE_F32X3) {
+                const bf16x8 alo = s == 0 ? c0_lo[i] : c1_lo[i];
+                acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc4[mb][nj], 0, 0, 0);
+                acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc4[mb][nj], 0, 0, 0);
+              }
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc4[mb][nj], 0, 0, 0);
             }
-            acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc4[mb][nj], 0, 0, 0);
           }
           if constexpr (blk < 2 * NX) xform_piece(std::integral_constant<int, tap + XT * (blk >> 1)>{},
                                                   std::integral_constant<int, blk & 1>{},
@@ -517,7 +534,158 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   SDP_T(3);
   // the direct 16x16 epilogue: every forward, and the data-gradient launches of the 16-wide tiles
   // and 2-wave workgroups (the LDS-staged epilogue below needs TC >= 32 and 4 waves)
-  if (SH == 16 && (!a.dact || TC < 32 || NW != 4)) {
+  if (TRANS && (!a.dact || TC < 32 || NW != 4)) {
+    if constexpr (TRANS) {
+    // ------------------------------------------------------------------ epilogue, 16x16 D = W x X
+    // Register r of fragment (mb, nj) of lane l holds Cout 16 nj + 4 (l / 16) + r of the wave's 64 at
+    // pixel l % 16 of the fragment's 16-px row segment: every load/store below moves 16 B per lane
+    // (a wave instruction covers 16 pixels x 64 B).  InstanceNorm++ statistics: the lane holds 8
+    // values (one per fragment mb) of each of its 16 channels; the 128-pixel group of a channel spans
+    // the 16 lanes of a DPP row -> per-lane two-pass (mean, M2), then Chan merges over the row by
+    // quad_perm / row_half_mirror / row_mirror moves.
+    __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
+    const int Ho = a.H, Wo = a.W;
+    const size_t bo = (size_t)b * Ho * Wo * Cout;
+    const int img_bytes = Ho * Wo * Cout * 4;
+    auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p + bo), 0, img_bytes, 0x00020000); };
+    const int lq = lane >> 4, lcol = lane & 15;
+    constexpr int CB = TC / 16;                      // 16-px fragments per tile row
+    const int voff = (lcol * d * Cout + 4 * lq) * 4; // lane part of every byte offset
+    auto soff = [&](int mb, int nj) {                // wave-uniform part: fragment mb's first pixel, channel block nj
+      const int mr = mb / CB, mc = (mb % CB) * 16;
+      const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc) * d + ph_c;
+      return __builtin_amdgcn_readfirstlane(((y * Wo + x) * Cout + n0 + wn * 64 + nj * 16) * 4);
+    };
+    auto ld = [&](__amdgpu_buffer_rsrc_t r, int so) {
+      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, voff, so, 0);
+      return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
+    };
+    auto st = [&](float4 v, __amdgpu_buffer_rsrc_t r, int so, auto aux_c) {
+      constexpr int AUX = decltype(aux_c)::value;
+      const u32x4 q = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+      __builtin_amdgcn_raw_buffer_store_b128(q, r, voff, so, AUX);
+    };
+    static_for<0, 4>([&](auto njc) {
+      constexpr int nj = decltype(njc)::value;
+      __builtin_amdgcn_sched_barrier(0);              // one channel block at a time (register pressure)
+      const int co0 = n0 + wn * 64 + nj * 16 + 4 * lq;   // the lane's 4 channels
+      const float4 bias4 = a.bias ? ld4(a.bias + co0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 esc = make_float4(1.f, 1.f, 1.f, 1.f), esh = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (a.dact == 3) {
+        const float4 s0 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2), s1 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2 + 4);
+        esc = make_float4(s0.x, s0.z, s1.x, s1.z);
+        esh = make_float4(s0.y, s0.w, s1.y, s1.w);
+      }
+      float4 v[8];
+      static_for<0, 8>([&](auto mbc) {
+        constexpr int mb = decltype(mbc)::value;
+        const f32x4 q = acc4[mb][nj];
+        v[mb] = make_float4(q[0] + bias4.x, q[1] + bias4.y, q[2] + bias4.z, q[3] + bias4.w);
+      });
+      if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor
+        const int Hi = a.H / 2, Wi = a.W / 2;
+        const float shh = (float)(Hi - 1) / (float)(a.H - 1), sww = (float)(Wi - 1) / (float)(a.W - 1);
+        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co0;
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb) {
+          const int mr = mb / CB, mc = (mb % CB) * 16;
+          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + lcol) * d + ph_c;
+          const float fy = shh * (float)y, fx = sww * (float)x;
+          const int y0 = (int)fy, x0 = (int)fx;
+          const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
+          const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+          const float4 v00 = ld4(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = ld4(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
+          const float4 v10 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
+          const float4 v11 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
+          auto bil = [&](float a00, float a01, float a10, float a11) {
+            return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+          };
+          v[mb].x = v[mb].x + bil(v00.x, v01.x, v10.x, v11.x);
+          v[mb].y = v[mb].y + bil(v00.y, v01.y, v10.y, v11.y);
+          v[mb].z = v[mb].z + bil(v00.z, v01.z, v10.z, v11.z);
+          v[mb].w = v[mb].w + bil(v00.w, v01.w, v10.w, v11.w);
+        }
+      }
+      if (a.dact) {   // backward: * the derivative of the ELU that followed this tensor (ConvArgs::dact)
+        static_for<0, 8>([&](auto mbc) {
+          constexpr int mb = decltype(mbc)::value;
+          float4 h = ld(rs(a.aux), soff(mb, nj));
+          if (a.dact == 3) h = make_float4(fmaf(h.x, esc.x, esh.x), fmaf(h.y, esc.y, esh.y), fmaf(h.z, esc.z, esh.z),
+                                           fmaf(h.w, esc.w, esh.w));
+          v[mb] = make_float4(v[mb].x * elu_grad(h.x, a.dact), v[mb].y * elu_grad(h.y, a.dact),
+                              v[mb].z * elu_grad(h.z, a.dact), v[mb].w * elu_grad(h.w, a.dact));
+        });
+      }
+      if (a.res) {
+        static_for<0, 8>([&](auto mbc) {
+          constexpr int mb = decltype(mbc)::value;
+          const float4 r = ld(rs(a.res), soff(mb, nj));
+          v[mb] = make_float4(r.x + v[mb].x, r.y + v[mb].y, r.z + v[mb].z, r.w + v[mb].w);
+        });
+      }
+      if (a.out2) {
+        static_for<0, 8>([&](auto mbc) {
+          constexpr int mb = decltype(mbc)::value;
+          const float4 r2 = ld(rs(a.res2), soff(mb, nj));
+          st(make_float4(v[mb].x + r2.x, v[mb].y + r2.y, v[mb].z + r2.z, v[mb].w + r2.w), rs(a.out2), soff(mb, nj),
+             std::integral_constant<int, 0>{});
+        });
+      }
+      if (a.epi_elu) {
+#pragma unroll
+        for (int mb = 0; mb < 8; ++mb) v[mb] = make_float4(elu(v[mb].x), elu(v[mb].y), elu(v[mb].z), elu(v[mb].w));
+      }
+      if constexpr (!(SDP_KO & 16)) {
+        static_for<0, 8>([&](auto mbc) {
+          constexpr int mb = decltype(mbc)::value;
+          st(v[mb], rs(a.out), soff(mb, nj), std::integral_constant<int, SDP_STORE_AUX>{});
+        });
+      }
+      if (a.stats) {
+        float mean[4], m2[4];
+        static_for<0, 4>([&](auto rc) {
+          constexpr int r = decltype(rc)::value;
+          auto comp = [&](const float4& q) { return r == 0 ? q.x : r == 1 ? q.y : r == 2 ? q.z : q.w; };
+          float s = 0.f;
+#pragma unroll
+          for (int mb = 0; mb < 8; ++mb) s += comp(v[mb]);
+          mean[r] = s * 0.125f;
+          float q2 = 0.f;
+#pragma unroll
+          for (int mb = 0; mb < 8; ++mb) {
+            const float dv = comp(v[mb]) - mean[r];
+            q2 = fmaf(dv, dv, q2);
+          }
+          m2[r] = q2;
+        });
+        // Chan merges of equal-count partials over the 16 lanes of the row: partners by lane ^ 1,
+        // lane ^ 2 (quad_perm), the mirrored quad (row_half_mirror), the mirrored half-row (row_mirror)
+        auto merge = [&](auto ctl_c, float n) {
+          constexpr int CTL = decltype(ctl_c)::value;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float mp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(mean[r]), CTL, 0xf, 0xf, false));
+            const float qp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(m2[r]), CTL, 0xf, 0xf, false));
+            const float dm = mean[r] - mp;
+            m2[r] = m2[r] + qp + dm * dm * (0.5f * n);
+            mean[r] = 0.5f * (mean[r] + mp);
+          }
+        };
+        merge(std::integral_constant<int, 0xB1>{}, 8.f);     // quad_perm [1,0,3,2]
+        merge(std::integral_constant<int, 0x4E>{}, 16.f);    // quad_perm [2,3,0,1]
+        merge(std::integral_constant<int, 0x141>{}, 32.f);   // row_half_mirror
+        merge(std::integral_constant<int, 0x140>{}, 64.f);   // row_mirror
+        if (lcol == 0) {
+          float4* sp = reinterpret_cast<float4*>(reinterpret_cast<float2*>(a.stats) +
+                                                 ((size_t)b * a.groups_per_img + tile * WM + wm) * Cout + co0);
+          sp[0] = make_float4(mean[0], m2[0], mean[1], m2[1]);
+          sp[1] = make_float4(mean[2], m2[2], mean[3], m2[3]);
+        }
+      }
+    });
+    }  // if constexpr (TRANS)
+  } else if (SH == 16 && !TRANS && (!a.dact || TC < 32 || NW != 4)) {
+    if constexpr (SH == 16 && !TRANS) {
     // ------------------------------------------------------------------ epilogue, 16x16 fragments
     // Register r of fragment (mb, nj) of lane l holds pixel 4 (l / 16) + r of the fragment's 16-px
     // row segment and Cout 16 nj + l % 16 of the wave's 64: every wave store writes four 64-B runs
@@ -647,6 +815,7 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
         }
       }
     });
+    }  // if constexpr (SH == 16 && !TRANS)
   } else if (a.dact) {
     if constexpr (TC >= 32 && NW == 4) {   // (TC = 16 tiles and 2-wave workgroups are forward-only, 16x16 shape)
     // data-gradient launches (training): the LDS-staged epilogue -- its 16-B pixel-row
@@ -696,7 +865,17 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
         // 16x16 fragments 4h .. 4h+3 of the wave hold the same 64 pixels as the 32x32 ones
         // 2h, 2h+1: fragment i, lane pixel 4 (l / 16) + r is staged pixel q = 16 i + 4 (l / 16) + r
         // (non-pooled only: the data-gradient launches; a pooled forward never takes this path)
-        if constexpr (!POOL) {
+        if constexpr (!POOL && TRANS) {   // lane l holds pixel l % 16, Couts 4 (l / 16) .. + 3: one 16-B write
+          static_for<0, 4>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            static_for<0, 4>([&](auto njc) {
+              constexpr int nj = decltype(njc)::value;
+              float* dst = stage + (wm * 64 + 16 * i + (lane & 15)) * SROW + wn * 64 + nj * 16 + 4 * (lane >> 4);
+              const f32x4 q = acc4[4 * h + i][nj];
+              *reinterpret_cast<float4*>(dst) = make_float4(q[0], q[1], q[2], q[3]);
+            });
+          });
+        } else if constexpr (!POOL) {
           static_for<0, 4>([&](auto ic) {
             constexpr int i = decltype(ic)::value;
             static_for<0, 4>([&](auto njc) {
