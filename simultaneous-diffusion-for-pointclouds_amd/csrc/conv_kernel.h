@@ -48,6 +48,12 @@ namespace sdp {
 #ifndef SDP_DMA_AUX
 #define SDP_DMA_AUX 0
 #endif
+// weight-ring depth of the bf16 16x16 launches (9 = a chunk ahead, 3 = two taps; A/B knob): the
+// 9-slot ring measured 135.5 -> 134.4 image-steps/s in the bf16 training step, so 3 stays
+// (profiles/experiments/r03_train_ring_wgrad_ab.log)
+#ifndef SDP_BF16_RING
+#define SDP_BF16_RING 3
+#endif
 #ifndef SDP_STORE_AUX
 #define SDP_STORE_AUX 2   // nt: the output streams to HBM without displacing the L2-resident weights
 #endif                    // (conv_bench 256->256 @32x512: 218 -> 214 us, tools/aux_run.sh)
@@ -180,7 +186,10 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
   // weight fragment ring: 3 taps deep (prefetch distance 2) when the tap count is a multiple
   // of 3, so the slot of (chunk, tap) is tap % 3 in every chunk; 2 deep for the 1x1 conv
-  constexpr int NBUF = (NT % 3 == 0) ? 3 : 2;
+  // bf16 mode on the 16x16 shape, SDP_BF16_RING=9: its hi-only fragments fit a ring of a whole chunk
+  // (9 slots, 8 taps ahead) in the registers fp32x3 spends on the lo halves (a tap is only 32 MFMAs
+  // there); measured slightly slower than the 3-slot ring, so off by default
+  constexpr int NBUF = (MODE == MODE_BF16 && SH == 16 && NT == 9 && SDP_BF16_RING == 9) ? 9 : ((NT % 3 == 0) ? 3 : 2);
   uint4 bq[NBUF][2][4];   // SH 32: [slot][nb][(s, hi/lo)]; SH 16: [slot][nj / 2][(nj % 2, hi/lo)]
   // SH 16: fragment nj (Couts 16 nj .. of the wave's 64) lane l needs Cout 16 nj + l % 16 and
   // channel group g = l / 16 (channels 8g .. 8g+7 of the chunk); the 32x32 packing stores Cout c,
@@ -348,7 +357,7 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   SDP_T(1);
   // ---- prologue: chunk 0 staged + transformed, chunk 1 in flight ----
   load_b(std::integral_constant<int, 0>{}, 0, 0);
-  if constexpr (NBUF == 3) load_b(std::integral_constant<int, 1>{}, 0, 1);
+  static_for<1, NBUF - 1>([&](auto j) { load_b(j, 0, decltype(j)::value); });
   load_ss(0);
   static_for<0, NU>([&](auto k) { load_unit(k, 0); });
   static_for<0, NU>([&](auto k) { xform_unit(k, std::integral_constant<int, 0>{}); });
@@ -394,8 +403,8 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
     static_for<0, NT>([&](auto tap_c) {
       constexpr int tap = decltype(tap_c)::value;
       constexpr int DIST = NBUF - 1;                       // prefetch distance in taps
-      constexpr int CUR = NBUF == 3 ? tap % 3 : (tap + P) & 1;
-      constexpr int NXT = NBUF == 3 ? (tap + DIST) % 3 : (tap + 1 + P) & 1;
+      constexpr int CUR = NBUF >= 3 ? tap % NBUF : (tap + P) & 1;
+      constexpr int NXT = NBUF >= 3 ? (tap + DIST) % NBUF : (tap + 1 + P) & 1;
       if constexpr (tap + DIST < NT) load_b(std::integral_constant<int, NXT>{}, chunk, tap + DIST);
       else load_b(std::integral_constant<int, NXT>{}, min(chunk + 1, nchunks - 1), tap + DIST - NT);
       __builtin_amdgcn_sched_barrier(0);

@@ -445,7 +445,7 @@ struct TrainPlan {
     // scratch (upper bounds over every layer of the network)
     wpart_n = (size_t)(WGRAD_TARGET_BLOCKS + 64) * 9 * 128 * 32;   // >= splits x 9 x Cin x Cout for every conv
     wpart = take(wpart_n);
-    spart = take((size_t)B * (H * W / 512) * 256 * 2);
+    spart = take((size_t)B * (H * W / 512) * 256 * 2);   // inpp_backward: 512-pixel groups (train_aux.hip INPP_GRP)
     coef = take((size_t)B * 256 * 4);
     bpart = take(1024 * 256);
     ppart = take((size_t)B * 256 * 3);

@@ -144,15 +144,19 @@ hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k,
 }
 
 // ---------------------------------------------------------------- InstanceNorm++ backward
-// part[b][grp][c] = (sum g, sum g * (h - mean) * rstd) over the 512 pixels of group grp
-__global__ __launch_bounds__(256) void inpp_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ h,
-                                                              const float4* __restrict__ nst, float2* __restrict__ part,
-                                                              int HW, int C) {
-  __shared__ float2 red[256 * 4];
+// part[b][grp][c] = (sum g, sum g * (h - mean) * rstd) over the INPP_GRP pixels of group grp.
+// 1024-thread blocks (4x the waves of 256-thread ones) with four independent loads in flight per
+// thread, so the reduce streams g and h at HBM rate while the finalize still sums only HW / 512
+// groups per image.
+constexpr int INPP_GRP = 512, INPP_NT = 1024;
+__global__ __launch_bounds__(INPP_NT) void inpp_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ h,
+                                                                  const float4* __restrict__ nst, float2* __restrict__ part,
+                                                                  int HW, int C) {
+  __shared__ float2 red[INPP_NT * 4];
   const int b = blockIdx.y, grp = blockIdx.x, ngrp = gridDim.x;
-  const int C4 = C / 4, PL = 256 / C4, tid = threadIdx.x;
+  const int C4 = C / 4, PL = INPP_NT / C4, tid = threadIdx.x;
   const int c4 = tid % C4, pl = tid / C4;
-  const size_t base = ((size_t)b * HW + (size_t)grp * 512) * C;
+  const size_t base = ((size_t)b * HW + (size_t)grp * INPP_GRP) * C;
   float4 mu, rs;
   {
     const float4 n0 = nst[(size_t)b * C + c4 * 4], n1 = nst[(size_t)b * C + c4 * 4 + 1];
@@ -161,19 +165,28 @@ __global__ __launch_bounds__(256) void inpp_bwd_reduce_kernel(const float* __res
     rs = make_float4(n0.y, n1.y, n2.y, n3.y);
   }
   float sg[4] = {0.f, 0.f, 0.f, 0.f}, sx[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int p = pl; p < 512; p += PL) {
-    const float4 gv = *reinterpret_cast<const float4*>(g + base + (size_t)p * C + c4 * 4);
-    const float4 hv = *reinterpret_cast<const float4*>(h + base + (size_t)p * C + c4 * 4);
-    sg[0] += gv.x; sg[1] += gv.y; sg[2] += gv.z; sg[3] += gv.w;
-    sx[0] = fmaf(gv.x, (hv.x - mu.x) * rs.x, sx[0]);
-    sx[1] = fmaf(gv.y, (hv.y - mu.y) * rs.y, sx[1]);
-    sx[2] = fmaf(gv.z, (hv.z - mu.z) * rs.z, sx[2]);
-    sx[3] = fmaf(gv.w, (hv.w - mu.w) * rs.w, sx[3]);
+  const int npp = INPP_GRP / PL;   // pixels per thread: 8 (C = 64) .. 64 (C = 512), a multiple of 4
+  for (int j = 0; j < npp; j += 4) {
+    float4 gv[4], hv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const size_t o = base + (size_t)(pl + (j + u) * PL) * C + c4 * 4;
+      gv[u] = *reinterpret_cast<const float4*>(g + o);
+      hv[u] = *reinterpret_cast<const float4*>(h + o);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sg[0] += gv[u].x; sg[1] += gv[u].y; sg[2] += gv[u].z; sg[3] += gv[u].w;
+      sx[0] = fmaf(gv[u].x, (hv[u].x - mu.x) * rs.x, sx[0]);
+      sx[1] = fmaf(gv[u].y, (hv[u].y - mu.y) * rs.y, sx[1]);
+      sx[2] = fmaf(gv[u].z, (hv[u].z - mu.z) * rs.z, sx[2]);
+      sx[3] = fmaf(gv[u].w, (hv[u].w - mu.w) * rs.w, sx[3]);
+    }
   }
 #pragma unroll
   for (int k = 0; k < 4; ++k) red[(pl * C4 + c4) * 4 + k] = make_float2(sg[k], sx[k]);
   __syncthreads();
-  for (int i = tid; i < C; i += 256) {
+  for (int i = tid; i < C; i += INPP_NT) {
     float a0 = 0.f, a1 = 0.f;
     for (int k = 0; k < PL; ++k) {
       const float2 v = red[(k * C4 + i / 4) * 4 + (i & 3)];
@@ -262,28 +275,35 @@ __global__ void inpp_bwd_params_kernel(const float* __restrict__ ppart, int B, i
   dbeta[c] = (float)be;
 }
 
-// out = k1*g + k2*(h - mean) + k3 (+ r1) (+ r2)
+// out = k1*g + k2*(h - mean) + k3 (+ r1) (+ r2).  Grid (blocks, B): a thread's channel group is
+// fixed (the block stride is a multiple of C/4), so its 4 coefficient rows are loaded once per image
 __global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ h,
                                                              const float4* __restrict__ coef, const float* r1,
-                                                             const float* r2, float* out, int HW, int C, size_t n4) {
+                                                             const float* r2, float* out, int HW, int C) {
   const int C4 = C / 4;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
-    const size_t b = i / C4 / HW;
-    const float4* cf = coef + b * C + c;
-    const float4 k0 = cf[0], kk1 = cf[1], kk2 = cf[2], kk3 = cf[3];
-    const float4 gv = reinterpret_cast<const float4*>(g)[i], hv = reinterpret_cast<const float4*>(h)[i];
+  const int b = blockIdx.y;
+  const size_t n4 = (size_t)HW * C4, off = (size_t)b * n4;
+  const size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  const int c = (int)(i0 % C4) * 4;
+  const float4* cf = coef + (size_t)b * C + c;
+  const float4 k0 = cf[0], kk1 = cf[1], kk2 = cf[2], kk3 = cf[3];
+  const float4* g4 = reinterpret_cast<const float4*>(g) + off;
+  const float4* h4 = reinterpret_cast<const float4*>(h) + off;
+  float4* o4 = reinterpret_cast<float4*>(out) + off;
+#pragma unroll 2
+  for (size_t i = i0; i < n4; i += stride) {
+    const float4 gv = g4[i], hv = h4[i];
     float4 v = make_float4(fmaf(k0.x, gv.x, fmaf(k0.y, hv.x - k0.w, k0.z)), fmaf(kk1.x, gv.y, fmaf(kk1.y, hv.y - kk1.w, kk1.z)),
                            fmaf(kk2.x, gv.z, fmaf(kk2.y, hv.z - kk2.w, kk2.z)), fmaf(kk3.x, gv.w, fmaf(kk3.y, hv.w - kk3.w, kk3.z)));
     if (r1) {
-      const float4 t = reinterpret_cast<const float4*>(r1)[i];
+      const float4 t = reinterpret_cast<const float4*>(r1)[off + i];
       v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
     }
     if (r2) {
-      const float4 t = reinterpret_cast<const float4*>(r2)[i];
+      const float4 t = reinterpret_cast<const float4*>(r2)[off + i];
       v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
     }
-    reinterpret_cast<float4*>(out)[i] = v;
+    o4[i] = v;
   }
 }
 
@@ -292,17 +312,19 @@ static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 25
 hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
                          int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
                          float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st) {
-  if (HW % 512 || C % 4 || C > 1024 || (256 % (C / 4))) return hipErrorInvalidValue;
-  const int ngrp = HW / 512;
-  hipLaunchKernelGGL(inpp_bwd_reduce_kernel, dim3(ngrp, B), dim3(256), 0, st, g, h,
+  if (HW % INPP_GRP || C % 4 || C > 512 || (256 % (C / 4)) || (INPP_GRP / (INPP_NT / (C / 4))) % 4) return hipErrorInvalidValue;
+  const int ngrp = HW / INPP_GRP;
+  hipLaunchKernelGGL(inpp_bwd_reduce_kernel, dim3(ngrp, B), dim3(INPP_NT), 0, st, g, h,
                      reinterpret_cast<const float4*>(nst), reinterpret_cast<float2*>(part), HW, C);
   hipLaunchKernelGGL(inpp_bwd_finalize_kernel, dim3(B), dim3(1024), 0, st, reinterpret_cast<const float2*>(part), ngrp,
                      (float)HW, reinterpret_cast<const float4*>(nst), alpha, gamma, C, reinterpret_cast<float4*>(coef),
                      ppart);
   hipLaunchKernelGGL(inpp_bwd_params_kernel, dim3((C + 255) / 256), dim3(256), 0, st, ppart, B, C, dalpha, dgamma, dbeta);
-  const size_t n4 = (size_t)B * HW * C / 4;
-  hipLaunchKernelGGL(inpp_bwd_apply_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, h,
-                     reinterpret_cast<const float4*>(coef), r1, r2, out, HW, C, n4);
+  // per image: 2048 blocks at most, the stride a multiple of C/4 (256 threads, C/4 divides 256)
+  const size_t n4 = (size_t)HW * C / 4;
+  const int nb = (int)std::min<size_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(inpp_bwd_apply_kernel, dim3(nb, B), dim3(256), 0, st, g, h,
+                     reinterpret_cast<const float4*>(coef), r1, r2, out, HW, C);
   return hipGetLastError();
 }
 

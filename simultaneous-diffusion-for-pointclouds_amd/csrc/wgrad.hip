@@ -47,8 +47,10 @@ struct WgTile {
   static constexpr int A_PLANE = NPIX * 64;             // [px][32 ci] bf16
 };
 
+// OCC: 1 = one workgroup per CU, next tile's loads in registers; 2 = two workgroups per CU taking
+// turns (chunked staging); 3 = one workgroup per CU with the next two tiles' loads in flight
 template <int MODE, int TC, int KS, int OCC>
-__global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
+__global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   using T = WgTile<TC, KS>;
   constexpr int NT = KS * KS;
@@ -72,8 +74,12 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
   });
 
-  float4 rd[T::NUD], ra[T::NUA];
+  // OCC 3: one workgroup per CU (512-register waves) with the global loads of the next TWO tiles in
+  // flight in two register sets, so a tile's load latency hides behind two tiles of MFMAs
+  constexpr int NSET = OCC == 3 ? 2 : 1;
+  float4 rdS[NSET][T::NUD], raS[NSET][T::NUA];
   int tb = 0, tph_r = 0, tph_c = 0, tsr0 = 0, tsc0 = 0;
+  int stb[NSET], ssr0[NSET], ssc0[NSET];   // the tile held by each register set (image, patch origin)
   auto decode = [&](int t) {
     tb = t / tiles_img;
     int r = t - tb * tiles_img;
@@ -116,8 +122,9 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
         ((((tsr0 - T::HALO) * d + tph_r) * a.W + (tsc0 - T::HALO) * d + tph_c) * Cin + ci0) * 4);
   };
   // global -> registers, units [KB, KE) of the dy tile / the input patch
-  auto load_dy = [&](auto kb_, auto ke_) {
-    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
+  auto load_dy = [&](auto kb_, auto ke_, auto set_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
+    float4* rd = rdS[SET];
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
       constexpr int KPR = TC / 8;
@@ -125,8 +132,9 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
       rd[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
     }
   };
-  auto load_a = [&](auto kb_, auto ke_) {
-    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
+  auto load_a = [&](auto kb_, auto ke_, auto set_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
+    float4* ra = raS[SET];
     if (interior) {
 #pragma unroll
       for (int k = KB; k < KE; ++k) {
@@ -168,8 +176,9 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
   };
   // registers -> LDS (prologue transform on the input patch, zero padding, bf16 split)
   float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);   // bias gradient: sum of dy over this thread's pixels
-  auto store_dy = [&](auto kb_, auto ke_) {
-    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
+  auto store_dy = [&](auto kb_, auto ke_, auto set_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
+    const float4* rd = rdS[SET];
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
       const int u = tid + k * 256, px = u >> 5, cv = u & 31;
@@ -180,9 +189,11 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
     // alive beside the next tile's loads (64 VGPRs of copies)
     asm volatile("" : "+v"(bsum.x), "+v"(bsum.y), "+v"(bsum.z), "+v"(bsum.w));
   };
-  auto store_a = [&](auto kb_, auto ke_) {
-    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value;
-    const float* ssb = a.pro_ss + (size_t)tb * a.ss_bstride + ci0 * 2;
+  auto store_a = [&](auto kb_, auto ke_, auto set_) {
+    constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
+    const float4* ra = raS[SET];
+    const int sb = OCC == 3 ? stb[SET] : tb, sr0_ = OCC == 3 ? ssr0[SET] : tsr0, sc0_ = OCC == 3 ? ssc0[SET] : tsc0;
+    const float* ssb = a.pro_ss + (size_t)sb * a.ss_bstride + ci0 * 2;
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
       const int u = tid + k * 256;
@@ -196,13 +207,14 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
         v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
       }
       if (!a.circular && KS == 3) {
-        const int sr = tsr0 - 1 + pix / T::PC, sc = tsc0 - 1 + pix % T::PC;
+        const int sr = sr0_ - 1 + pix / T::PC, sc = sc0_ - 1 + pix % T::PC;
         if (sr < 0 || sr >= Hs || sc < 0 || sc >= Ws) v = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       put_bf16(aL, T::A_PLANE, pix * 64 + cv * 8, v);
     }
   };
   using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
   using IND = std::integral_constant<int, T::NUD>;
   using INA = std::integral_constant<int, T::NUA>;
   // OCC 2: two workgroups per CU take turns (one stages while the other's MFMAs run), so a
@@ -212,14 +224,14 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
     static_for<0, (T::NUD + CH - 1) / CH>([&](auto c) {
       using KB = std::integral_constant<int, decltype(c)::value * CH>;
       using KE = std::integral_constant<int, (decltype(c)::value * CH + CH < T::NUD ? decltype(c)::value * CH + CH : T::NUD)>;
-      load_dy(KB{}, KE{});
-      store_dy(KB{}, KE{});
+      load_dy(KB{}, KE{}, I0{});
+      store_dy(KB{}, KE{}, I0{});
     });
     static_for<0, (T::NUA + CH - 1) / CH>([&](auto c) {
       using KB = std::integral_constant<int, decltype(c)::value * CH>;
       using KE = std::integral_constant<int, (decltype(c)::value * CH + CH < T::NUA ? decltype(c)::value * CH + CH : T::NUA)>;
-      load_a(KB{}, KE{});
-      store_a(KB{}, KE{});
+      load_a(KB{}, KE{}, I0{});
+      store_a(KB{}, KE{}, I0{});
     });
   };
 
@@ -231,30 +243,8 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
   const char* dy_rd = dyL + wave * (128 * 64) + mcol * 2;
   const char* a_rd = aL + mcol * 2;
 
-  if (OCC == 1 && t_begin < t_end) {
-    decode(t_begin);
-    prep_tile();
-    load_dy(I0{}, IND{});
-    load_a(I0{}, INA{});
-  }
-  for (int t = t_begin; t < t_end; ++t) {
-    __syncthreads();
-    if constexpr (OCC == 1) {
-      store_dy(I0{}, IND{});
-      store_a(I0{}, INA{});
-      __syncthreads();
-      if (t + 1 < t_end) {
-        decode(t + 1);
-        prep_tile();
-        load_dy(I0{}, IND{});
-        load_a(I0{}, INA{});
-      }
-    } else {
-      decode(t);
-      prep_tile();
-      stage_chunked();
-      __syncthreads();
-    }
+  // the MFMAs of the staged tile: 8 k steps of 16 pixels x all taps
+  auto compute = [&]() __attribute__((always_inline)) {
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {   // 16 pixels per k step
       const int k0 = 16 * s + kq, k1 = k0 + 4;
@@ -285,6 +275,61 @@ __global__ __launch_bounds__(256, OCC) void conv_wgrad_kernel(WgradArgs a) {
         }
         acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[tap], 0, 0, 0);
       });
+    }
+  };
+  // OCC 3: load tile tt into register set SET (and remember its coordinates for the LDS store)
+  auto fetch_set = [&](auto set_, int tt) __attribute__((always_inline)) {
+    constexpr int SET = decltype(set_)::value;
+    decode(tt);
+    prep_tile();
+    stb[SET] = tb;
+    ssr0[SET] = tsr0;
+    ssc0[SET] = tsc0;
+    load_dy(I0{}, IND{}, set_);
+    load_a(I0{}, INA{}, set_);
+  };
+  auto step3 = [&](auto set_, int t) __attribute__((always_inline)) {
+    __syncthreads();   // the previous tile's MFMAs are done with the LDS tiles
+    store_dy(I0{}, IND{}, set_);
+    store_a(I0{}, INA{}, set_);
+    __syncthreads();
+    if (t + 2 < t_end) fetch_set(set_, t + 2);
+    compute();
+  };
+
+  if constexpr (OCC == 3) {
+    if (t_begin < t_end) fetch_set(I0{}, t_begin);
+    if (t_begin + 1 < t_end) fetch_set(I1{}, t_begin + 1);
+    for (int t = t_begin; t < t_end; t += 2) {
+      step3(I0{}, t);
+      if (t + 1 < t_end) step3(I1{}, t + 1);
+    }
+  } else {
+    if (OCC == 1 && t_begin < t_end) {
+      decode(t_begin);
+      prep_tile();
+      load_dy(I0{}, IND{}, I0{});
+      load_a(I0{}, INA{}, I0{});
+    }
+    for (int t = t_begin; t < t_end; ++t) {
+      __syncthreads();
+      if constexpr (OCC == 1) {
+        store_dy(I0{}, IND{}, I0{});
+        store_a(I0{}, INA{}, I0{});
+        __syncthreads();
+        if (t + 1 < t_end) {
+          decode(t + 1);
+          prep_tile();
+          load_dy(I0{}, IND{}, I0{});
+          load_a(I0{}, INA{}, I0{});
+        }
+      } else {
+        decode(t);
+        prep_tile();
+        stage_chunked();
+        __syncthreads();
+      }
+      compute();
     }
   }
   // bias partials (the ci-block-0 workgroups): bpart[split][Cout]; every thread's channel
@@ -346,26 +391,50 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   *o = accumulate ? *o + s : s;
 }
 
+// staging scheme of the bf16 weight gradient (A/B knob SDP_WGRAD_OCC = 2 | 3 | 1; fp32x3 runs OCC 1).
+// Two workgroups per CU (2) beat one with the next two tiles' loads in flight (3) and one with the
+// next tile's (1): 134.4 vs 119.2 vs 119.2 image-steps/s in the bf16 training step
+// (profiles/experiments/r03_train_ring_wgrad_ab.log)
+static int wgrad_occ_bf16() {
+  static const int o = [] {
+    const char* e = getenv("SDP_WGRAD_OCC");
+    return e ? atoi(e) : 2;
+  }();
+  return o;
+}
+
 int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks) {
   const int tc = ((W / d) % 64 == 0) ? 64 : 32;
   const int total = B * (H / d) * (W / d) / 128 * d * d;
   (void)tc;
   const int blocks = (Cin / 32) * (Cout / 128);
-  int S = (WGRAD_TARGET_BLOCKS + blocks - 1) / blocks;
+  // (the one-workgroup-per-CU scheme of the bf16 weight gradient aims at one round of 256; the
+  // split count also sizes the partial buffer, so it depends only on this process-wide knob)
+  const int target = wgrad_occ_bf16() == 3 ? WGRAD_TARGET_BLOCKS / 2 : WGRAD_TARGET_BLOCKS;
+  int S = (target + blocks - 1) / blocks;
   S = S < total ? S : total;
   return S < 1 ? 1 : S;
 }
 
 size_t wgrad_part_floats(int S, int Cin, int Cout, int ks) { return (size_t)S * ks * ks * Cin * Cout; }
 
-template <int MODE>
-static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
-  dim3 grid(S, a.Cin / 32, a.Cout / 128);
-  constexpr int OCC = MODE == MODE_BF16 ? 2 : 1;
+template <int MODE, int OCC>
+static hipError_t wgrad_occ(const WgradArgs& a, int ks, int tc, dim3 grid, hipStream_t st) {
   if (ks == 1) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 1, OCC>), grid, dim3(256), 0, st, a);
   else if (tc == 64) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3, OCC>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3, OCC>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
+  dim3 grid(S, a.Cin / 32, a.Cout / 128);
+  if constexpr (MODE == MODE_BF16) {
+    if (wgrad_occ_bf16() == 3) return wgrad_occ<MODE, 3>(a, ks, tc, grid, st);
+    if (wgrad_occ_bf16() == 1) return wgrad_occ<MODE, 1>(a, ks, tc, grid, st);
+    return wgrad_occ<MODE, 2>(a, ks, tc, grid, st);
+  }
+  return wgrad_occ<MODE, 1>(a, ks, tc, grid, st);
 }
 
 hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,
