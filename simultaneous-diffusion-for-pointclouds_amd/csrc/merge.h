@@ -30,6 +30,8 @@ struct MergeArgs {
   uint32_t* tcount;        // [T][nchunk], scanned in place
   uint32_t* bsum;          // scan block totals
   float4* rec;             // [pairs]: (code as 2 floats' bits, intensity, s << 10 | column)
+  int32_t* pcell;          // [pairs]: K1's projection of every pair (big-grid cell or -1) and its
+  double* pcode;           //   depth code, so K3 scatters without projecting again (same bits)
   int nchunk;
   float* newimg;           // [n_out][2][HW]
   uint8_t* maskimg;        // [n_out][HW]

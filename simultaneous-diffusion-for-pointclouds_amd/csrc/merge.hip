@@ -103,10 +103,12 @@ __device__ __noinline__ Proj project(const MergeArgs& a, double4 w, int o) {
 // scattered addresses), and every pair needs four (count, two sums, nearest code): a 32-view
 // megabatch spent 3.8 ms of an 18.8-ms step there.  Instead the pairs are binned by
 // destination tile = (output view, big-grid row):
-//   K1 bin_count  : each chunk of pairs projects its points and counts them per tile (LDS);
+//   K1 bin_count  : each chunk of pairs projects its points, counts them per tile (LDS) and keeps
+//                   every pair's (cell, code) -- the float64 projection (two atan2, log2, sqrt)
+//                   is the costly part of both binning passes;
 //   scan          : exclusive offsets over [tile][chunk] (tile-major);
-//   K3 bin_scatter: the chunks project again and write one 16-B record per pair into their
-//                   tile's range (LDS cursors);
+//   K3 bin_scatter: the chunks read the kept projections back and write one 16-B record per pair
+//                   into their tile's range (LDS cursors);
 //   K4 segments   : workgroups take 4096 consecutive (so tile-sorted) records, sum them per
 //                   cell in LDS (ds atomics) and add each touched cell to the grids once, with
 //                   contiguous lanes; a second sweep finds the lowest source index among the
@@ -131,7 +133,11 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
     int ol, s, o, m0;
     pair_of(a, i, HW, ol, s, o, m0);
     const Proj pr = project(a, a.world[(size_t)m0 * HW + s], o);
-    if (pr.cell >= 0) atomicAdd(&hist[ol * a.g.big + pr.cell / a.g.W], 1u);
+    a.pcell[i] = pr.cell;
+    if (pr.cell >= 0) {
+      a.pcode[i] = pr.code;
+      atomicAdd(&hist[ol * a.g.big + pr.cell / a.g.W], 1u);
+    }
   }
   __syncthreads();
   for (int t = threadIdx.x; t < T; t += 256) a.tcount[(size_t)t * a.nchunk + blockIdx.x] = hist[t];
@@ -149,10 +155,13 @@ __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, siz
   const size_t n = (size_t)a.n_out * a.aB * HW;
   const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
   for (size_t i = i0 + threadIdx.x; i < i1; i += 256) {
+    const int cell = a.pcell[i];
+    if (cell < 0) continue;
     int ol, s, o, m0;
     pair_of(a, i, HW, ol, s, o, m0);
-    const Proj pr = project(a, a.world[(size_t)m0 * HW + s], o);
-    if (pr.cell < 0) continue;
+    Proj pr;
+    pr.cell = cell;
+    pr.code = a.pcode[i];
     const int row = pr.cell / a.g.W, col = pr.cell % a.g.W;
     const uint32_t pos = atomicAdd(&cur[ol * a.g.big + row], 1u);
     const float inten = a.x[((size_t)m0 * 2 + 1) * HW + (size_t)(s / HW) * 2 * HW + (s % HW)];
@@ -410,6 +419,8 @@ size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   add(nt * 4);                                               // tcount
   add(((nt + 2047) / 2048 + 1) * 4);                         // bsum
   add(npair * 16);                                           // records
+  add(npair * 4);                                            // pcell
+  add(npair * 8);                                            // pcode
   add((size_t)n_out * 2 * H * W * 4);                        // newimg (internal)
   add((size_t)n_out * H * W);                                // maskimg
   return b + 1024;
@@ -439,6 +450,8 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   a.tcount = reinterpret_cast<uint32_t*>(take(nt * 4));
   a.bsum = reinterpret_cast<uint32_t*>(take(((nt + 2047) / 2048 + 1) * 4));
   a.rec = reinterpret_cast<float4*>(take(npair * 16));
+  a.pcell = reinterpret_cast<int32_t*>(take(npair * 4));
+  a.pcode = reinterpret_cast<double*>(take(npair * 8));
   a.newimg = new_out ? new_out : reinterpret_cast<float*>(take((size_t)a.n_out * 2 * H * W * 4));
   a.maskimg = reinterpret_cast<uint8_t*>(take((size_t)a.n_out * H * W));
   const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
