@@ -43,8 +43,8 @@ extern "C" {
 /* arithmetic used for the score network's convolutions (fp32 I/O and accumulation in all modes) */
 enum sdp_precision {
   SDP_PREC_FP32 = 0,    /* v_mfma_f32_32x32x2_f32: exact fp32 products                         */
-  SDP_PREC_FP32X3 = 1,  /* 3-pass bf16 split (hi*hi + hi*lo + lo*hi): forward on                  */
-                        /* v_mfma_f32_16x16x32_bf16, data gradient on v_mfma_f32_32x32x16_bf16   */
+  SDP_PREC_FP32X3 = 1,  /* 3-pass bf16 split (hi*hi + hi*lo + lo*hi) on v_mfma_f32_16x16x32_bf16  */
+                        /* (forward and data gradient; weight gradient on v_mfma_f32_32x32x16)   */
   SDP_PREC_BF16 = 2     /* single bf16 pass (fast, NOT within the fp32 parity tolerance)        */
 };
 

@@ -64,7 +64,7 @@ struct Proj {
   double code;  // log2(d+1)/6*smod
 };
 
-// project world point w into output view o (global index); noinline so K1 and K2 agree bitwise
+// project world point w into output view o (global index); K1 keeps the result for K3 (pcell, pcode)
 __device__ __noinline__ Proj project(const MergeArgs& a, double4 w, int o) {
   Proj pr;
   pr.cell = -1;
