@@ -999,6 +999,36 @@ hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, con
   return hipGetLastError();
 }
 
+// 2x2 mean pool of the ConvMeanPool 1x1 shortcut's input (layers.py:291-313 with the mean taken before the
+// 1x1 conv instead of after it: the conv is linear per pixel, so the two orders differ only in float
+// rounding, and the conv then runs on a quarter of the pixels).  Summation order of layers.py:311-312:
+// ((x[::2, ::2] + x[1::2, ::2]) + x[::2, 1::2]) + x[1::2, 1::2], then / 4.
+__global__ __launch_bounds__(256) void avgpool2_kernel(const float4* __restrict__ in, float4* __restrict__ out, int H,
+                                                       int W, int C4, size_t n4) {
+  const int Ho = H / 2, Wo = W / 2;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4);
+    size_t p = i / C4;
+    const int x = (int)(p % Wo);
+    p /= Wo;
+    const int y = (int)(p % Ho);
+    const size_t b = p / Ho;
+    const size_t r0 = ((b * H + 2 * y) * W + 2 * x) * C4 + c, r1 = r0 + (size_t)W * C4;
+    const float4 a00 = in[r0], a01 = in[r0 + C4], a10 = in[r1], a11 = in[r1 + C4];
+    out[i] = make_float4((((a00.x + a10.x) + a01.x) + a11.x) / 4.0f, (((a00.y + a10.y) + a01.y) + a11.y) / 4.0f,
+                         (((a00.z + a10.z) + a01.z) + a11.z) / 4.0f, (((a00.w + a10.w) + a01.w) + a11.w) / 4.0f);
+  }
+}
+
+hipError_t avgpool2(const float* in, float* out, int B, int H, int W, int C, hipStream_t st) {
+  if ((H & 1) || (W & 1) || (C & 3)) return hipErrorInvalidValue;
+  const size_t n4 = (size_t)B * (H / 2) * (W / 2) * (C / 4);
+  const int grid = (int)std::min<size_t>((n4 + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(avgpool2_kernel, dim3(grid), dim3(256), 0, st, reinterpret_cast<const float4*>(in),
+                     reinterpret_cast<float4*>(out), H, W, C / 4, n4);
+  return hipGetLastError();
+}
+
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
   if (C % 128 || W % MP_COLS) return hipErrorInvalidValue;
   auto blocks = [&](int rows) { return B * ((H + rows - 1) / rows) * (W / MP_COLS) * (C / 128); };

@@ -29,7 +29,8 @@ static int half_wg() {   // 0 = off, 1 = 128-channel outputs, 2 = also the 256-c
 
 template <int MODE, bool PELU>
 static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, bool half, hipStream_t st) {
-  if (ks == 1) return conv_launch<MODE, 1, 64, 1, true, PELU>(a, st);   // only the ConvMeanPool 1x1 shortcut
+  if (ks == 1)   // the ConvMeanPool 1x1 shortcut: pooled epilogue (training), or on pre-pooled input (forward)
+    return pool ? conv_launch<MODE, 1, 64, 1, true, PELU>(a, st) : conv_launch<MODE, 1, 64, 1, false, PELU>(a, st);
   if (pool) return conv_launch<MODE, 1, 64, 3, true, PELU>(a, st);
   if constexpr (MODE != MODE_F32) {   // 16-wide tiles: the 16x16 MFMA shape only
 #ifndef SDP_CONV_BENCH_ONLY
@@ -112,7 +113,7 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (ks == 1 || pool) tc = 64;
   const int tr = wm * 128 / tc;
   if (Ws % tc || Hs % tr) { *why = "conv: sub-grid not divisible by the pixel tile"; return hipErrorInvalidValue; }
-  if (ks == 1 && !pool) { *why = "conv: 1x1 only as the pooled shortcut"; return hipErrorInvalidValue; }
+  if (ks == 1 && !pool && (d != 1 || wm != 1)) { *why = "conv: 1x1 needs d=1 and 256-multiple Cout"; return hipErrorInvalidValue; }
   if (pool && (d != 1 || wm != 1 || (a.H & 1) || (a.W & 1))) {
     *why = "conv: pooling needs d=1, even H,W and 256-multiple Cout";
     return hipErrorInvalidValue;

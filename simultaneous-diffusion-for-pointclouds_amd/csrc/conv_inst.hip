@@ -2,7 +2,7 @@
 //
 // Built once per kernel shape (Makefile: conv_i_<code>.o with -DSDP_INST=<code>):
 //   forward : code = 100 * (mode + 1) + 10 * pelu + shape   (shape = index into FwdShape; 7 = the
-//             2-wave workgroups of conv_launch_half)
+//             2-wave workgroups of conv_launch_half; 8 = the non-pooled 1x1)
 //   dgrad   : code = 1000 + 10 * mode + shape                (shape = index into DgradShape)
 // Without SDP_INST (tools/conv_bench, -DSDP_CONV_BENCH_ONLY) it instantiates the 3x3 non-pooled
 // ELU-prologue forward shapes of every mode, which is all that bench dispatches.
@@ -89,6 +89,7 @@ template <> struct FwdShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; s
 template <> struct FwdShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool POOL = false; };
 template <> struct FwdShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
 template <> struct FwdShape<6> { static constexpr int WM = 2, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
+template <> struct FwdShape<8> { static constexpr int WM = 1, TC = 64, KS = 1; static constexpr bool POOL = false; };  // pool-first 1x1 shortcut
 template <int MODE>
 hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st) {
   using T = ConvTile<1, 16, 3, 2>;
@@ -113,7 +114,8 @@ static_assert(kMode >= 1 && kMode <= 2 && kPelu <= 1, "SDP_INST: bad 2-wave forw
 template hipError_t conv_launch_half<kMode, (kPelu != 0)>(ConvArgs, hipStream_t);
 #elif defined(SDP_INST) && SDP_INST < 1000
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
-static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && kShape <= 6 && (kShape < 5 || kMode != MODE_F32),
+static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && (kShape <= 6 || kShape == 8) &&
+                  (kShape < 5 || kShape == 8 || kMode != MODE_F32),
               "SDP_INST: bad forward code");
 using FS = FwdShape<kShape>;
 template hipError_t conv_launch<kMode, FS::WM, FS::TC, FS::KS, FS::POOL, (kPelu != 0)>(ConvArgs, hipStream_t);

@@ -17,6 +17,8 @@ hipError_t end_conv(const float* in, const float* ss, const float* w, const floa
 hipError_t inpp_finalize(const float* stats, int B, int T, float cnt, int C, const float* alpha, const float* gamma,
                          const float* beta, float* ss, hipStream_t st, float* nst, void* scratch);
 hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx = nullptr);
+// 2x2 mean pool (the pool-first ConvMeanPool 1x1 shortcut): out [B][H/2][W/2][C]
+hipError_t avgpool2(const float* in, float* out, int B, int H, int W, int C, hipStream_t st);
 hipError_t langevin_step(float* x, const float* g, const float* ref, const int32_t* mask, const float* noise,
                          uint64_t seed, uint64_t offset, float step, float nscale, float gref, int n2n, int B, int C,
                          int HW, float* lik_out, uint32_t* absmax, hipStream_t st);

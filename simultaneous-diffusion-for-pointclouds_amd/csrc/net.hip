@@ -144,11 +144,15 @@ struct Fwd {
     o2.stats = want_stats;
     o2.dil = dil;
     if (down && dil == 1) {
-      // ConvMeanPool shortcut (1x1, zero pad) on the raw input, then conv2 = ConvMeanPool 3x3
+      // ConvMeanPool shortcut (1x1) pool-first: the 2x2 mean of the raw input (into `out`, free until
+      // conv2 writes it), then the 1x1 conv at half resolution (a quarter of the FLOPs of conv-then-pool;
+      // the same linear map, float rounding aside); then conv2 = ConvMeanPool 3x3
+      const Buf xp{out.p, x.H / 2, x.W / 2, x.C};
+      prof_launch("avgpool2 " + std::to_string(x.C) + " @" + std::to_string(x.H) + "x" + std::to_string(x.W),
+                  1.25 * B * x.H * x.W * x.C * 4, [&] { chk(avgpool2(x.p, xp.p, B, x.H, x.W, x.C, st), "avgpool2"); });
       Opt os;
       os.circular = false;
-      os.pool = true;
-      conv(x, k + ".shortcut.conv", t2, os);
+      conv(xp, k + ".shortcut.conv", t2, os);
       o2.circular = false;
       o2.pool = true;
       o2.res = t2.p;
