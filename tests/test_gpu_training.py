@@ -67,7 +67,12 @@ def test_training_forward_matches_inference_forward(case):
     a = tr.forward(x, y)
     b = net(x, y)
     torch.cuda.synchronize()
-    assert torch.equal(a, b)
+    # the sampling forward takes the ConvMeanPool 1x1 shortcut pool-first (2x2 mean, then the conv at
+    # half resolution; linear, so it differs from the training tape's conv-then-pool only in rounding):
+    # equal within the score-net parity tolerance (1e-4 of max|out|)
+    err = ((a - b).abs().max() / b.abs().max()).item()
+    print(f"training vs sampling forward: max err / max|out| = {err:.3e}")
+    assert err < 1e-4
 
 
 def test_dsm_loss_and_gradients_match_oracle(case):
