@@ -65,7 +65,20 @@ struct Proj {
 };
 
 // project world point w into output view o (global index); K1 keeps the result for K3 (pcell, pcode)
-__device__ __noinline__ Proj project(const MergeArgs& a, double4 w, int o) {
+// project() inlined into the count pass: merge 450 -> 398 us at a 32-view megabatch (one config-4
+// rank), 170 -> 156 us at 4 views (profiles/experiments/r03_merge_inline_ab.log); 0 = a call
+#ifndef SDP_MERGE_INLINE
+#define SDP_MERGE_INLINE 1
+#endif
+#ifndef SDP_MERGE_UNROLL   // pairs per thread and iteration of the count pass (world loads issued together)
+#define SDP_MERGE_UNROLL 1
+#endif
+#if SDP_MERGE_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+Proj project(const MergeArgs& a, double4 w, int o) {
   Proj pr;
   pr.cell = -1;
   pr.code = 0.0;
@@ -129,14 +142,26 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
   __syncthreads();
   const size_t n = (size_t)a.n_out * a.aB * HW;
   const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
-  for (size_t i = i0 + threadIdx.x; i < i1; i += 256) {
-    int ol, s, o, m0;
-    pair_of(a, i, HW, ol, s, o, m0);
-    const Proj pr = project(a, a.world[(size_t)m0 * HW + s], o);
-    a.pcell[i] = pr.cell;
-    if (pr.cell >= 0) {
-      a.pcode[i] = pr.code;
-      atomicAdd(&hist[ol * a.g.big + pr.cell / a.g.W], 1u);
+  constexpr int U = SDP_MERGE_UNROLL;
+  for (size_t i = i0 + threadIdx.x; i < i1; i += 256 * U) {
+    int ol[U], s[U], o[U], m0[U];
+    double4 wv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {   // clamped pair index: every load unconditional
+      const size_t ii = min(i + 256 * u, i1 - 1);
+      pair_of(a, ii, HW, ol[u], s[u], o[u], m0[u]);
+      wv[u] = a.world[(size_t)m0[u] * HW + s[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t ii = i + 256 * u;
+      if (ii >= i1) break;
+      const Proj pr = project(a, wv[u], o[u]);
+      a.pcell[ii] = pr.cell;
+      if (pr.cell >= 0) {
+        a.pcode[ii] = pr.code;
+        atomicAdd(&hist[ol[u] * a.g.big + pr.cell / a.g.W], 1u);
+      }
     }
   }
   __syncthreads();
@@ -401,7 +426,12 @@ __global__ __launch_bounds__(256) void merge_apply_kernel(MergeArgs a) {
 static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 256 * 16); }
 
 // pair chunks of the binning passes: ~1024 (4 per CU), at least 2048 pairs each
-static int merge_chunks(size_t npair) { return (int)std::max<size_t>(1, std::min<size_t>(1024, (npair + 2047) / 2048)); }
+#ifndef SDP_MERGE_CHUNK_MAX   // A/B knob: most workgroups of the count / scatter passes
+#define SDP_MERGE_CHUNK_MAX 1024
+#endif
+static int merge_chunks(size_t npair) {
+  return (int)std::max<size_t>(1, std::min<size_t>(SDP_MERGE_CHUNK_MAX, (npair + 2047) / 2048));
+}
 
 size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   const int big = (int)((25 * 2) * (long)H / 28);
