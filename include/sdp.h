@@ -94,7 +94,7 @@ int sdp_net_forward_langevin(sdp_net* net, float* x, const int64_t* labels, int 
                              void* workspace, size_t workspace_bytes, void* stream);
 /* Performance knob: run sdp_net_forward / sdp_net_forward_langevin as `ways` part-batch forwards on
  * that many streams (the caller's + the handle's own, joined before return; 1 = one launch per
- * layer, 0 = the default: env SDP_SPLIT, else 2).  Results are identical for every value; the
+ * layer, 0 = the default, 2).  Results are identical for every value; the
  * workspace size depends on it (query sdp_net_workspace_size after setting it).              */
 int sdp_net_set_split(sdp_net* net, int ways);
 /* Measurement hooks: when enabled, every conv launch of sdp_net_forward is bracketed by HIP

@@ -281,6 +281,37 @@ def gen_kitti_e2e():
     save("kitti_e2e_b2_64x256.npz", new=imgs[0].numpy(), new2=imgs[1].numpy(), final=imgs[2].numpy())
 
 
+# AllForOne sampler loop end to end: (setting, minStepToShare).  Setting 5 ramps cc = (c+1)/L over
+# the 3 levels (models/__init__.py:209-212) and, with minStepToShare 0, keeps the level-0 shared
+# images (L505-506); setting 7 is the controlled average the AllForOne runner uses (AllForOne:589).
+ALLFORONE_E2E = [(5, 0), (7, 1)]
+
+
+def gen_allforone_e2e():
+    """anneal_Langevin_dynamics_inpainting_simultaneous_basic (models/__init__.py:112-602) end to end:
+    B=aB=3 origins (Circle.yml's first three), ngf=128 net, 3 late levels x 2 steps + denoise (64x256)."""
+    models = _ref_imports()
+    H, W, B = 64, 256, 3
+    m = build_net(128, H, W)
+    sig = get_sigmas_np()[229:232]
+    for setting, min_step in ALLFORONE_E2E:
+        tag = f"a_e2e_set{setting}"
+        case = GI.merge_case(tag, B, H, W)
+        x0 = GI.scorenet_input(tag, B, H, W)
+        with torch.no_grad(), _NoiseFeed(tag):
+            imgs, _, shared = models.anneal_Langevin_dynamics_inpainting_simultaneous_basic(
+                torch.from_numpy(x0), torch.from_numpy(case["ref"]), torch.from_numpy(case["mask"]),
+                torch.from_numpy(case["sky"]), None, min_step, setting, m, sig,
+                torch.from_numpy(np.array(CIRCLE_MODS[:B])), B, n_steps_each=2, step_lr=6.2e-6,
+                existMask=torch.from_numpy(case["exist"]), denoise=True, verbose=False, grad_ref=1,
+                correlation_coefficient=0.01)
+        # images = [newImages (last level, step 1), (step 2), final x]; shared = level-0 newImages (L505-508)
+        assert len(imgs) == 3 and len(shared) == (2 if min_step == 0 else 0)
+        extra = {"shared0": shared[0].numpy(), "shared1": shared[1].numpy()} if shared else {}
+        save(f"allforone_e2e_set{setting}_b3_64x256.npz", new=imgs[0].numpy(), new2=imgs[1].numpy(),
+             final=imgs[2].numpy(), **extra)
+
+
 def gen_dsm():
     """Masked DSM loss (losses/dsm.py:67-119) + parameter-gradient norms, ngf=128 at 64x128, B=2."""
     sys.path.insert(0, REF)
@@ -319,9 +350,10 @@ def gen_projection():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     what = sys.argv[1:] or ["exist", "scorenet", "ops", "langevin", "merge", "allforone", "config1", "e2e", "dsm",
-                            "projection", "allforone9", "big"]
+                            "projection", "allforone9", "big", "allforone_e2e"]
     _ref_imports()
     for w in what:
         {"exist": gen_exist, "scorenet": gen_scorenet, "ops": gen_ops, "langevin": gen_langevin,
          "merge": gen_merge, "allforone": gen_allforone, "config1": gen_config1, "e2e": gen_kitti_e2e,
-         "dsm": gen_dsm, "projection": gen_projection, "allforone9": gen_allforone9, "big": gen_big}[w]()
+         "dsm": gen_dsm, "projection": gen_projection, "allforone9": gen_allforone9, "big": gen_big,
+         "allforone_e2e": gen_allforone_e2e}[w]()

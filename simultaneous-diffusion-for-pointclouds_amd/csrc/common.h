@@ -61,9 +61,10 @@ SDP_DEV float elu_grad(float t, int form) {
 // Arguments of one implicit-GEMM 3x3 / 1x1 convolution launch (activations NHWC float32).
 struct ConvArgs {
   const float* in;         // [B][H][W][Cin]
-  const uint4* wf;         // fragment-ordered weights (see net.cpp pack_conv_weights)
-  const uint4* wf16;       // forward weights in 16x16 fragment order (train_aux.hip pack_slot16), or null
-  const uint4* wfw;        // Winograd F(2,3)-transformed weights in 16x16 fragment order (wino_kernel.h), or null
+  const uint4* wf;         // 32x32 fragment-ordered weights (train_aux.hip pack_slot): the exact-fp32
+                           //   forward "#frag" and every data gradient "#dfrag"
+  const uint4* wf16;       // forward weights in 16x16 fragment order "#frag16" (train_aux.hip
+                           //   pack_slot16): the bf16-mode forward
   const float* bias;       // [Cout] or null
   float* out;              // [B][Ho][Wo][Cout]  (Ho,Wo = H,W or H/2,W/2 when pooled)
   const float* res;        // residual, layout of out, or null
@@ -108,13 +109,8 @@ struct WgradArgs {
 // together on an XCD a full-height block: their halos (and the circular wrap of the top and bottom
 // rows) are each other's pixels, read once into that XCD's L2, instead of re-read by the next
 // round's row of tiles: 256 -> 256 @32x512 reads 125 -> 108 MB per launch (HBM traffic 1.40 -> 1.25x
-// the algorithmic bytes), time unchanged.  0 (row-major) when SDP_STRIP=0.
+// the algorithmic bytes), time unchanged (profiles/experiments/r03_strip_ab.log).
 inline int conv_strip_w(int tile_rows, int tile_cols) {
-  static const int on = [] {
-    const char* e = getenv("SDP_STRIP");
-    return e ? atoi(e) : 1;
-  }();
-  if (!on) return 0;
   int sw = 1;
   while (sw * 2 * tile_rows <= 32 && tile_cols % (sw * 2) == 0) sw *= 2;
   return sw;

@@ -6,8 +6,6 @@
 // (conv_kernel.h) run on dy with the "dgrad" weight packing (train_aux.hip pack kernel),
 // without prologue, and with the backward epilogue: *elu'(...) of the forward activation
 // (ConvArgs::dact) and the residual add of the gradient already accumulated for its input.
-#include <cstdlib>
-
 #include "conv_launch.h"
 
 // preferred tile width of the 128 px x 256 Cout data-gradient workgroups (A/B knob; the forward's is
@@ -20,17 +18,11 @@ namespace sdp {
 
 // 8 x 16 pixel tiles (the forward's: a 10 x 18 patch, 1.41x the pixels, against 4 x 66 = 2.06x for
 // the 2 x 64 tiles) with the transposed direct 16x16 epilogue (conv_kernel.h TRN: 16-B elu' operand,
-// residual and output accesses) -- the 128-channel outputs on 2-wave workgroups.  The default since
-// the transposed epilogue: bf16 training step 132.8 -> 137.0 image-steps/s (with 4-B accesses it was
-// 60.5 -> 64.3 ms slower; profiles/experiments/r03_dgrad16_train_ab.log, r03_trans_ab.log).
-// SDP_DGRAD16=0 keeps the 2 x 64 tiles with the LDS-staged epilogue.
-static bool dgrad16() {
-  static const bool on = [] {
-    const char* e = getenv("SDP_DGRAD16");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return on;
-}
+// residual and output accesses) -- the 128-channel outputs on 2-wave workgroups -- wherever the
+// sub-grid tiles into 8 x 16 (every circular 3x3 layer of the network): bf16 training step 132.8 ->
+// 137.0 image-steps/s against the 2 x 64 tiles (profiles/experiments/r03_dgrad16_train_ab.log,
+// r03_trans_ab.log).  The zero-padded and 1x1 layers keep 2 x 64 / 8 x 32 tiles with the LDS-staged
+// epilogue.
 
 template <int MODE>
 static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, bool t16, hipStream_t st) {
@@ -60,9 +52,8 @@ hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char**
   if (a.dact && !a.aux) { *why = "dgrad: dact needs aux"; return hipErrorInvalidValue; }
   if (a.dact == 3 && !a.epi_ss) { *why = "dgrad: dact 3 needs epi_ss"; return hipErrorInvalidValue; }
   if (!a.pro_ss) { *why = "dgrad: prologue identity table missing"; return hipErrorInvalidValue; }
-  // 16-wide tiles: the 16x16 MFMA shape (the default; SDP_DGRAD_SHAPE=32 keeps the 32x32 one)
-  const char* shp = getenv("SDP_DGRAD_SHAPE");
-  const bool t16 = dgrad16() && !(shp && atoi(shp) == 32) && ks == 3 && a.circular && Ws % 16 == 0 && Hs % 8 == 0;
+  if (!a.wf || a.wf16) { *why = "dgrad: weights in wf (the #dfrag packing), wf16 null"; return hipErrorInvalidValue; }
+  const bool t16 = ks == 3 && a.circular && Ws % 16 == 0 && Hs % 8 == 0;
   switch (mode) {
     case MODE_F32X3: return launch_dgrad_mode<MODE_F32X3>(a, ks, wm, tc, t16, st);
     case MODE_BF16: return launch_dgrad_mode<MODE_BF16>(a, ks, wm, tc, t16, st);

@@ -3,34 +3,19 @@
 // Built once per kernel shape (Makefile: conv_i_<code>.o with -DSDP_INST=<code>):
 //   forward : code = 100 * (mode + 1) + 10 * pelu + shape   (shape = index into FwdShape; 7 = the
 //             2-wave workgroups of conv_launch_half; 8 = the non-pooled 1x1)
+//   dgrad 2-wave workgroups: code = 1000 + 10 * mode + 6
 //   dgrad   : code = 1000 + 10 * mode + shape                (shape = index into DgradShape)
 // Without SDP_INST (tools/conv_bench, -DSDP_CONV_BENCH_ONLY) it instantiates the 3x3 non-pooled
 // ELU-prologue forward shapes of every mode, which is all that bench dispatches.
-#include <cstdlib>
-
 #include "conv_kernel.h"
 #include "conv_launch.h"
 
 namespace sdp {
 
-// MFMA shape of the forward bf16-mode launches (conv_kernel.h SH): 16 unless SDP_MFMA_SHAPE=32
-static int mfma_shape() {
-  static const int sh = [] {
-    const char* e = getenv("SDP_MFMA_SHAPE");
-    return (e && atoi(e) == 32) ? 32 : 16;
-  }();
-  return sh;
-}
-
-// MFMA shape of the data-gradient launches (the LDS-staged epilogue handles both): 16 unless
-// SDP_DGRAD_SHAPE=32
-static int dgrad_shape() {
-  static const int sh = [] {
-    const char* e = getenv("SDP_DGRAD_SHAPE");
-    return (e && atoi(e) == 32) ? 32 : 16;
-  }();
-  return sh;
-}
+// MFMA shapes: the bf16 modes (fp32x3, bf16) run every launch on v_mfma_f32_16x16x32_bf16 (SH = 16);
+// exact fp32 on v_mfma_f32_32x32x2_f32 (SH = 32).  The 16x16 shape holds a higher clock under this
+// power-limited load at the same cycles per FLOP (256->256 185 -> 171 us,
+// 128->128 @64x1024 227 -> 214 us).
 
 template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
 hipError_t conv_launch(ConvArgs a, hipStream_t st) {
@@ -40,16 +25,13 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   a.strip_w = conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / TC);
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   if constexpr (MODE != MODE_F32) {
-    if (!a.dact && mfma_shape() == 16) {
-      hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16>), grid, dim3(256), 0, st, a);
-      return hipGetLastError();
-    }
-  }
-  if constexpr (TC >= 32) {   // the 32x32 shape tiles rows in 32-pixel fragments
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+  } else if constexpr (TC >= 32) {   // the 32x32 shape tiles rows in 32-pixel fragments
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
   }
-  return hipErrorInvalidValue;   // (not reached: conv.hip picks 16-wide tiles for the 16x16 forward only)
+  return hipErrorInvalidValue;   // (not reached: conv.hip picks 16-wide tiles for the bf16 modes only)
 }
 
 template <int MODE, bool PELU>
@@ -72,10 +54,8 @@ hipError_t dgrad_launch(ConvArgs a, hipStream_t st) {
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   if constexpr (TC < 32) {   // 8 x 16 tiles: the transposed direct epilogue (conv_kernel.h TRN)
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16, 4, true>), grid, dim3(256), 0, st, a);
-  } else if (dgrad_shape() == 16) {
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }
@@ -88,7 +68,6 @@ template <> struct FwdShape<2> { static constexpr int WM = 2, TC = 32, KS = 3; s
 template <> struct FwdShape<3> { static constexpr int WM = 1, TC = 64, KS = 3; static constexpr bool POOL = false; };
 template <> struct FwdShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool POOL = false; };
 template <> struct FwdShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
-template <> struct FwdShape<6> { static constexpr int WM = 2, TC = 16, KS = 3; static constexpr bool POOL = false; };  // 16x16 shape only
 template <> struct FwdShape<8> { static constexpr int WM = 1, TC = 64, KS = 1; static constexpr bool POOL = false; };  // pool-first 1x1 shortcut
 template <int MODE>
 hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st) {
@@ -114,7 +93,7 @@ static_assert(kMode >= 1 && kMode <= 2 && kPelu <= 1, "SDP_INST: bad 2-wave forw
 template hipError_t conv_launch_half<kMode, (kPelu != 0)>(ConvArgs, hipStream_t);
 #elif defined(SDP_INST) && SDP_INST < 1000
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10, kShape = SDP_INST % 10;
-static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && (kShape <= 6 || kShape == 8) &&
+static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && (kShape <= 5 || kShape == 8) &&
                   (kShape < 5 || kShape == 8 || kMode != MODE_F32),
               "SDP_INST: bad forward code");
 using FS = FwdShape<kShape>;
@@ -130,16 +109,12 @@ static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16
 using DS = DgradShape<kShape>;
 template hipError_t dgrad_launch<kMode, DS::WM, DS::TC, DS::KS, DS::ZP>(ConvArgs, hipStream_t);
 #elif defined(SDP_CONV_BENCH_ONLY)
-#define SDP_BENCH_INST(M)                                                           \
-  template hipError_t conv_launch<M, 2, 32, 3, false, true>(ConvArgs, hipStream_t); \
-  template hipError_t conv_launch<M, 1, 64, 3, false, true>(ConvArgs, hipStream_t); \
-  template hipError_t conv_launch<M, 1, 32, 3, false, true>(ConvArgs, hipStream_t);
-SDP_BENCH_INST(MODE_F32)
-SDP_BENCH_INST(MODE_F32X3)
-SDP_BENCH_INST(MODE_BF16)
+template hipError_t conv_launch<MODE_F32, 2, 32, 3, false, true>(ConvArgs, hipStream_t);
+template hipError_t conv_launch<MODE_F32, 1, 32, 3, false, true>(ConvArgs, hipStream_t);
+template hipError_t conv_launch<MODE_F32X3, 1, 16, 3, false, true>(ConvArgs, hipStream_t);
+template hipError_t conv_launch<MODE_BF16, 1, 16, 3, false, true>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_half<MODE_F32X3, true>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_half<MODE_BF16, true>(ConvArgs, hipStream_t);
-#undef SDP_BENCH_INST
 #else
 #error "conv_inst.hip: build with -DSDP_INST=<code> (Makefile) or -DSDP_CONV_BENCH_ONLY (tools/conv_bench)"
 #endif

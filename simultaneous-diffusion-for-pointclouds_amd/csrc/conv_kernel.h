@@ -48,12 +48,6 @@ namespace sdp {
 #ifndef SDP_DMA_AUX
 #define SDP_DMA_AUX 0
 #endif
-// weight-ring depth of the bf16 16x16 launches (9 = a chunk ahead, 3 = two taps; A/B knob): the
-// 9-slot ring measured 135.5 -> 134.4 image-steps/s in the bf16 training step, so 3 stays
-// (profiles/experiments/r03_train_ring_wgrad_ab.log)
-#ifndef SDP_BF16_RING
-#define SDP_BF16_RING 3
-#endif
 #ifndef SDP_STORE_AUX
 #define SDP_STORE_AUX 2   // nt: the output streams to HBM without displacing the L2-resident weights
 #endif                    // (conv_bench 256->256 @32x512: 218 -> 214 us, tools/aux_run.sh)
@@ -106,9 +100,9 @@ SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p);
 // 209 -> 213 us) while the bf16 training step ran 132.8 -> 137.0 image-steps/s with the transposed
 // direct epilogue on the data gradient (profiles/experiments/r03_trans_ab.log).
 template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4, bool TRN = false>
-__global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) {
+__global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
-  static_assert(SH == 32 || (SH == 16 && MODE != MODE_F32), "16x16 shape: bf16 modes only");
+  static_assert((SH == 32) == (MODE == MODE_F32), "bf16 modes: 16x16 shape; exact fp32: 32x32");
   static_assert(NW == 4 || (SH == 16 && !POOL), "2-wave workgroups: the 16x16 non-pooled forward only");
   using T = ConvTile<WM, TC, KS, NW>;
   constexpr int NTH = T::NTH;
@@ -177,19 +171,19 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
 
   // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
   // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
-  // SH 16 forward: the 16x16-native packing "#frag16" when present (every fragment load of a wave
-  // reads 1 KiB contiguous), else the 32x32 packing read in 16-B pieces per lane
-  const bool c16 = SH == 16 && !a.dact && a.wf16;
+  // SH 16 forward: the 16x16-native packing "#frag16" in wf16 (every fragment load of a wave reads
+  // 1 KiB contiguous); the data gradient (wf16 null, conv_dgrad checks it) reads the 32x32 "#dfrag"
+  // packing in wf in 16-B pieces per lane
+  const bool c16 = SH == 16 && a.wf16 != nullptr;
   const __amdgpu_buffer_rsrc_t wrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(c16 ? a.wf16 : a.wf), 0, 0x7fffffff, 0x00020000);
   const int wv0 = ((nbg0 + 0) * 64 + lane) * 64, wv1 = ((nbg0 + 1) * 64 + lane) * 64;
   typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
   // weight fragment ring: 3 taps deep (prefetch distance 2) when the tap count is a multiple
-  // of 3, so the slot of (chunk, tap) is tap % 3 in every chunk; 2 deep for the 1x1 conv
-  // bf16 mode on the 16x16 shape, SDP_BF16_RING=9: its hi-only fragments fit a ring of a whole chunk
-  // (9 slots, 8 taps ahead) in the registers fp32x3 spends on the lo halves (a tap is only 32 MFMAs
-  // there); measured slightly slower than the 3-slot ring, so off by default
-  constexpr int NBUF = (MODE == MODE_BF16 && SH == 16 && NT == 9 && SDP_BF16_RING == 9) ? 9 : ((NT % 3 == 0) ? 3 : 2);
+  // of 3, so the slot of (chunk, tap) is tap % 3 in every chunk; 2 deep for the 1x1 conv (a 9-slot
+  // ring for the hi-only bf16 fragments measured 135.5 -> 134.4 image-steps/s in the bf16 training
+  // step, profiles/experiments/r03_train_ring_wgrad_ab.log)
+  constexpr int NBUF = (NT % 3 == 0) ? 3 : 2;
   uint4 bq[NBUF][2][4];   // SH 32: [slot][nb][(s, hi/lo)]; SH 16: [slot][nj / 2][(nj % 2, hi/lo)]
   // SH 16: fragment nj (Couts 16 nj .. of the wave's 64) lane l needs Cout 16 nj + l % 16 and
   // channel group g = l / 16 (channels 8g .. 8g+7 of the chunk); the 32x32 packing stores Cout c,
@@ -210,14 +204,12 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
     if constexpr (SDP_KO & 4) return;
     const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096);
     // (the lo halves only in fp32x3: MODE_BF16 multiplies the hi parts alone)
-    if constexpr (SH == 32) {
+    if constexpr (SH == 32) {   // exact fp32: 16 fp32 k values of a 32-Cout block per lane
       static_for<0, 4>([&](auto q) {
-        if constexpr (MODE != MODE_BF16 || (decltype(q)::value & 1) == 0) {
-          const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
-          const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
-          bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
-          bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
-        }
+        const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv0 + q * 16, so, 0);
+        const u32x4 v1 = __builtin_amdgcn_raw_buffer_load_b128(wrs, wv1 + q * 16, so, 0);
+        bq[J][0][q] = make_uint4(v0.x, v0.y, v0.z, v0.w);
+        bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
       });
     } else {
       static_for<0, 4>([&](auto njc) {
@@ -237,7 +229,6 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   // consumed only by the next chunk's transform, so the loads stay in flight across a chunk
   const float* ssb = a.pro_ss + (size_t)b * a.ss_bstride;
   const int my_cv = tid & 7;                        // every unit of a thread has cv == tid % 8
-  const int a_lane_off = (lane & 31) * PSTRIDE + (lane >> 5) * 16;
   float4 ssv0, ssv1;                                // (scale, shift) of this thread's 4 channels
   auto load_ss = [&](int chunk) __attribute__((always_inline)) {
     ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
@@ -368,27 +359,18 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
   __syncthreads();
   SDP_T(2);
 
-  // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel.
-  // SH 32: s = the 16-deep k step, fragments mb 0..3 (32 px each); SH 16: s = which half of the 8
-  // 16-px fragments (mb 4s .. 4s+3), lane l = pixel l % 16, channels 8 (l / 16) ..
+  // A fragments of (tap, s) for the bf16 modes: lane reads 16 B = 8 channels of one patch pixel;
+  // s = which half of the 8 16-px fragments (mb 4s .. 4s+3), lane l = pixel l % 16, channels 8 (l / 16) ..
   const int a_lane_off16 = (lane & 15) * PSTRIDE + (lane >> 4) * 16;
   auto read_a = [&](const char* pat, auto tap_c, auto s_c, bf16x8* hi, bf16x8* lo) __attribute__((always_inline)) {
     constexpr int tap = decltype(tap_c)::value, s = decltype(s_c)::value;
     constexpr int kh = (KS == 3) ? tap / 3 : 0, kw = (KS == 3) ? tap % 3 : 0;
     static_for<0, 4>([&](auto mbc) {
-      if constexpr (SH == 32) {
-        constexpr int mb = decltype(mbc)::value;
-        constexpr int mr = mb / (TC / 32), mc = (mb % (TC / 32)) * 32;
-        const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off + s * 32;
-        hi[mb] = *reinterpret_cast<const bf16x8*>(src);
-        if constexpr (MODE == MODE_F32X3) lo[mb] = *reinterpret_cast<const bf16x8*>(src + 64);
-      } else {
-        constexpr int i = decltype(mbc)::value, mb = 4 * s + i;
-        constexpr int mr = mb / (TC / 16), mc = (mb % (TC / 16)) * 16;
-        const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off16;
-        hi[i] = *reinterpret_cast<const bf16x8*>(src);
-        if constexpr (MODE == MODE_F32X3) lo[i] = *reinterpret_cast<const bf16x8*>(src + 64);
-      }
+      constexpr int i = decltype(mbc)::value, mb = 4 * s + i;
+      constexpr int mr = mb / (TC / 16), mc = (mb % (TC / 16)) * 16;
+      const char* src = pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off16;
+      hi[i] = *reinterpret_cast<const bf16x8*>(src);
+      if constexpr (MODE == MODE_F32X3) lo[i] = *reinterpret_cast<const bf16x8*>(src + 64);
     });
   };
 
@@ -477,22 +459,10 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
         if constexpr (tap + 1 < NT)
           read_a(pat, std::integral_constant<int, tap + 1>{}, std::integral_constant<int, 0>{}, pre_hi, pre_lo);
         if constexpr (NT > 1) dmas();   // 1x1: after the blocks, behind this tap's raw reads
-        constexpr int NBLK = SH == 32 ? 16 : 32;
+        constexpr int NBLK = 32;
         static_for<0, NBLK>([&](auto blk_c) {
           constexpr int blk = decltype(blk_c)::value;
-          if constexpr (SH == 32) {
-            constexpr int s = blk >> 3, nb = (blk >> 2) & 1, mb = blk & 3;
-            const uint4 h4 = bq[CUR][nb][2 * s], l4 = bq[CUR][nb][2 * s + 1];
-            const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
-            const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
-            const bf16x8 ahi = s == 0 ? c0_hi[mb] : c1_hi[mb];
-            if constexpr (MODE == MODE_F32X3) {
-              const bf16x8 alo = s == 0 ? c0_lo[mb] : c1_lo[mb];
-              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[mb][nb], 0, 0, 0);
-              acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[mb][nb], 0, 0, 0);
-            }
-            acc[mb][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[mb][nb], 0, 0, 0);
-          } else {
+          {
             // block = (half s of the px groups, Cout group nj, px group i of the half)
             constexpr int s = blk >> 4, nj = (blk >> 2) & 3, i = blk & 3, mb = 4 * s + i;
             const uint4 h4 = bq[CUR][nj >> 1][2 * (nj & 1)], l4 = bq[CUR][nj >> 1][2 * (nj & 1) + 1];
@@ -826,7 +796,7 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
     });
     }  // if constexpr (SH == 16 && !TRANS)
   } else if (a.dact) {
-    if constexpr (TC >= 32 && NW == 4) {   // (TC = 16 tiles and 2-wave workgroups are forward-only, 16x16 shape)
+    if constexpr (TC >= 32 && NW == 4 && SH == 16) {   // (the data gradient runs in the bf16 modes only)
     // data-gradient launches (training): the LDS-staged epilogue -- its 16-B pixel-row
     // accesses of the elu' operand and the residual gradient beat per-channel 4-B accesses
     // ------------------------------------------------------------------ epilogue
@@ -859,18 +829,7 @@ __global__ __launch_bounds__(64 * NW, 4 / NW) void conv_mfma_kernel(ConvArgs a) 
     static_for<0, 2>([&](auto hc) {
       constexpr int h = decltype(hc)::value;
       // ---- stage this half's accumulators: wave (wm, wn), fragments mb of the half
-      if constexpr (SH == 32) {
-        static_for<0, 2>([&](auto ic) {
-          constexpr int mb = POOL ? (h + 2 * decltype(ic)::value) : (2 * h + decltype(ic)::value);
-          constexpr int q0 = decltype(ic)::value * 32;
-          static_for<0, 2>([&](auto nbc) {
-            constexpr int nb = decltype(nbc)::value;
-            float* dst = stage + (wm * 64 + q0 + 4 * (lane >> 5)) * SROW + wn * 64 + nb * 32 + (lane & 31);
-  #pragma unroll
-            for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * SROW] = acc[mb][nb][r];
-          });
-        });
-      } else {
+      {
         // 16x16 fragments 4h .. 4h+3 of the wave hold the same 64 pixels as the 32x32 ones
         // 2h, 2h+1: fragment i, lane pixel 4 (l / 16) + r is staged pixel q = 16 i + 4 (l / 16) + r
         // (non-pooled only: the data-gradient launches; a pooled forward never takes this path)

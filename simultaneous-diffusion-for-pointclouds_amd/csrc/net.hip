@@ -52,9 +52,9 @@ struct Fwd {
     const auto& hp = net->host.at(wkey + ".weight");
     ConvArgs a{};
     a.in = in.p;
-    a.wf = reinterpret_cast<const uint4*>(net->P(wkey + ".weight#frag"));
-    a.wfw = net->wino_w(wkey);
-    a.wf16 = getenv("SDP_FRAG16") && atoi(getenv("SDP_FRAG16")) == 0 ? nullptr : net->frag16_w(wkey);
+    // forward weights: "#frag16" in the bf16 modes (16x16 MFMAs), "#frag" for exact fp32 (32x32)
+    a.wf = net->mode == MODE_F32 ? reinterpret_cast<const uint4*>(net->P(wkey + ".weight#frag")) : nullptr;
+    a.wf16 = net->mode == MODE_F32 ? nullptr : reinterpret_cast<const uint4*>(net->P(wkey + ".weight#frag16"));
     a.bias = o.bias ? net->P(wkey + ".bias") : nullptr;
     a.out = out.p;
     a.res = o.res;
@@ -319,17 +319,10 @@ static size_t workspace_bytes_one(const sdp_net* net, int B) {
   return r((size_t)B * (H * W / 64) * C2 * 2) + r((size_t)B * C2 * 2) + r((size_t)B * C2 * 4) + 6 * r(F) + 8 * r(Q);
 }
 
-// default of sdp_net::split: SDP_SPLIT=k runs the forward as k part-batch forwards on k streams
-// (forward_split); 1 = off
-static int split_default() {
-  static const int k = [] {
-    const char* e = getenv("SDP_SPLIT");
-    const int v = e ? atoi(e) : 2;
-    return v < 1 ? 1 : (v > SDP_MAX_SPLIT ? SDP_MAX_SPLIT : v);
-  }();
-  return k;
-}
-static int split_ways(const sdp_net* net) { return net->split > 0 ? net->split : split_default(); }
+// default of sdp_net::split: two part-batch forwards on two streams (forward_split; the A/B that
+// set it: profiles/experiments/r02_split_streams_ab.log)
+constexpr int kSplitDefault = 2;
+static int split_ways(const sdp_net* net) { return net->split > 0 ? net->split : kSplitDefault; }
 
 // part p of B images split k ways: [first, first + count)
 static void split_part(int B, int k, int p, int& first, int& count) {
@@ -398,18 +391,6 @@ static void forward_split(sdp_net* net, const float* x, const int64_t* labels, f
     if (p) chk(hipEventRecord(net->ev_join[p - 1], s), "hipEventRecord");
   }
   for (int p = 0; p + 1 < k; ++p) chk(hipStreamWaitEvent(st, net->ev_join[p], 0), "hipStreamWaitEvent");
-}
-
-// SDP_GRAPH=1 turns on the forward's HIP-graph replay (never while profiling).  Off by default:
-// measured at 4 views the replay and the plain launch sequence run the same step time
-// (315.2 vs 315.4 image-steps/s) -- the ~130 launches per forward are issued far ahead of the GPU,
-// so the inter-kernel gaps are already small.
-static bool graphs_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("SDP_GRAPH");
-    return e && e[0] == '1';
-  }();
-  return on;
 }
 
 // ------------------------------------------------------------------------------ C ABI
@@ -531,7 +512,6 @@ int sdp_net_bind_params(sdp_net* net, float* arena, void* stream) {
       chk(hipMemcpyAsync(arena, net->arena, net->arena_floats * 4, hipMemcpyDeviceToDevice, st), "hipMemcpyAsync");
     chk(hipStreamSynchronize(st), "hipStreamSynchronize");
     if (net->arena_owned) chk(hipFree(net->arena), "hipFree");
-    net->drop_graphs();                              // captured forwards read the old arena
     net->arena = arena;
     net->arena_owned = false;
     for (auto& e : net->layout) net->dev[e.key] = arena + e.offset;
@@ -564,54 +544,7 @@ int sdp_net_forward(sdp_net* net, const float* x, const int64_t* labels, float* 
   if (ws_bytes < workspace_bytes(net, B)) return fail("sdp_net_forward: workspace too small");
   const hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   try {
-    if (net->profile || !graphs_enabled()) {
-      forward_split(net, x, labels, out, B, ws, ws_bytes, st, nullptr);
-      return 0;
-    }
-    // HIP-graph replay: ~130 launches per forward cost one graph launch; the captured kernels
-    // read the labels from lab_dev, refreshed by a small copy on the caller's stream
-    if (net->lab_cap < B) {
-      if (net->lab_dev) {
-        chk(hipStreamSynchronize(st), "hipStreamSynchronize");   // replays in flight read lab_dev
-        chk(hipFree(net->lab_dev), "hipFree");
-      }
-      net->drop_graphs();
-      chk(hipMalloc(&net->lab_dev, (size_t)B * sizeof(int64_t)), "hipMalloc labels");
-      net->lab_cap = B;
-    }
-    chk(hipMemcpyAsync(net->lab_dev, labels, (size_t)B * sizeof(int64_t), hipMemcpyDeviceToDevice, st), "copy labels");
-    sdp_net::GraphEntry* g = nullptr;
-    for (auto& e : net->graphs)
-      if (e.x == x && e.out == out && e.B == B && e.ws == ws) g = &e;
-    if (!g) {
-      if (!net->cap_stream) chk(hipStreamCreateWithFlags(&net->cap_stream, hipStreamNonBlocking), "hipStreamCreate");
-      hipGraph_t graph = nullptr;
-      chk(hipStreamBeginCapture(net->cap_stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-      try {
-        forward_impl(net, x, net->lab_dev, out, B, ws, ws_bytes, net->cap_stream);
-      } catch (...) {
-        (void)hipStreamEndCapture(net->cap_stream, &graph);
-        if (graph) (void)hipGraphDestroy(graph);
-        throw;
-      }
-      chk(hipStreamEndCapture(net->cap_stream, &graph), "hipStreamEndCapture");
-      hipGraphExec_t exec = nullptr;
-      const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-      (void)hipGraphDestroy(graph);
-      chk(e, "hipGraphInstantiate");
-      if (net->graphs.size() >= 4) {                 // evict the least recently used
-        auto lru = net->graphs.begin();
-        for (auto it = net->graphs.begin(); it != net->graphs.end(); ++it)
-          if (it->used < lru->used) lru = it;
-        chk(hipStreamSynchronize(st), "hipStreamSynchronize");
-        (void)hipGraphExecDestroy(lru->exec);
-        net->graphs.erase(lru);
-      }
-      net->graphs.push_back({x, out, B, ws, exec, 0});
-      g = &net->graphs.back();
-    }
-    g->used = ++net->graph_clock;
-    chk(hipGraphLaunch(g->exec, st), "hipGraphLaunch");
+    forward_split(net, x, labels, out, B, ws, ws_bytes, st, nullptr);
   } catch (const std::exception& e) {
     return fail(std::string("sdp_net_forward: ") + e.what());
   }

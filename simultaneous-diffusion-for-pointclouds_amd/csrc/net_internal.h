@@ -47,7 +47,8 @@ struct sdp_net {
   std::vector<hipEvent_t> ev_pool;
   std::map<std::string, sdp::HostParam> host;
   // device tensors: parameters (pointers into `arena`), "sigmas", "#ident_ss" and the packed
-  // conv weights "<key>#frag" (forward) / "<key>#dfrag" (data gradient, training only)
+  // conv weights "<key>#frag16" (forward, bf16 modes) or "<key>#frag" (forward, exact fp32) and
+  // "<key>#dfrag" (data gradient, training only)
   std::map<std::string, void*> dev;
   std::vector<sdp::ParamEntry> layout;
   float* arena = nullptr;           // every learnable parameter, fp32, `layout` order
@@ -57,39 +58,17 @@ struct sdp_net {
   bool train_packs = false;         // keep the dgrad packings current in repack()
   int mode = sdp::MODE_F32X3;
   sdp::TrainPlan* plan = nullptr;   // tape of the last sdp_net_forward_train
-  // forward replays: the launch sequence captured once per (x, out, B, workspace) into a HIP
-  // graph (labels are copied into lab_dev first, so they are not part of the key); a few
-  // entries, least recently used evicted
-  struct GraphEntry {
-    const void* x;
-    void* out;
-    int B;
-    void* ws;
-    hipGraphExec_t exec;
-    unsigned long long used;
-  };
-  std::vector<GraphEntry> graphs;
-  unsigned long long graph_clock = 0;
-  hipStream_t cap_stream = nullptr;
-  int split = 0;                     // part-batch forwards (0: SDP_SPLIT, default 2)
+  int split = 0;                     // part-batch forwards (0: the default, 2)
   hipStream_t aux_stream[sdp::SDP_MAX_SPLIT - 1] = {};   // part-batch forwards 1.. (net.hip forward_split)
   hipEvent_t ev_fork = nullptr, ev_join[sdp::SDP_MAX_SPLIT - 1] = {};
-  int64_t* lab_dev = nullptr;       // [lab_cap] labels of the replayed forwards
-  int lab_cap = 0;
-  void drop_graphs() {
-    for (auto& g : graphs) (void)hipGraphExecDestroy(g.exec);
-    graphs.clear();
-  }
 
   ~sdp_net() {
     release();
-    if (cap_stream) (void)hipStreamDestroy(cap_stream);
     for (auto& s : aux_stream)
       if (s) (void)hipStreamDestroy(s);
     for (auto& e : ev_join)
       if (e) (void)hipEventDestroy(e);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (lab_dev) (void)hipFree(lab_dev);
     for (auto& r : prof) {
       (void)hipEventDestroy(r.a);
       (void)hipEventDestroy(r.b);
@@ -97,7 +76,6 @@ struct sdp_net {
     for (auto e : ev_pool) (void)hipEventDestroy(e);
   }
   void release() {
-    drop_graphs();
     for (auto& kv : dev) {
       const bool in_arena = arena && kv.second >= (void*)arena && kv.second < (void*)(arena + arena_floats);
       if (!in_arena) (void)hipFree(kv.second);
@@ -122,14 +100,6 @@ struct sdp_net {
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) throw std::runtime_error("hipEventCreate");
     return e;
-  }
-  const uint4* wino_w(const std::string& wkey) const {   // "#wfrag" of a 3x3 conv, or null
-    auto it = dev.find(wkey + ".weight#wfrag");
-    return it == dev.end() ? nullptr : reinterpret_cast<const uint4*>(it->second);
-  }
-  const uint4* frag16_w(const std::string& wkey) const {   // "#frag16" (bf16 modes), or null
-    auto it = dev.find(wkey + ".weight#frag16");
-    return it == dev.end() ? nullptr : reinterpret_cast<const uint4*>(it->second);
   }
   const float* P(const std::string& k) const {
     auto it = dev.find(k);
@@ -156,15 +126,16 @@ struct sdp_net {
     for (auto& kv : host) {
       if (!is_conv_w(kv.first)) continue;
       const auto& s = kv.second.shape;
-      // packings: 0 = forward "#frag", 1 = data gradient "#dfrag" (training), 2 = the Winograd
-      // F(2,3) forward "#wfrag" of the 3x3 convs (bf16 modes; 12 transformed taps), 3 = the forward
-      // in 16x16 fragment order "#frag16" (bf16 modes)
+      // packings: 0 = forward "#frag" (32x32 fragment order: the exact-fp32 forward), 1 = data
+      // gradient "#dfrag" (training), 3 = the forward in 16x16 fragment order "#frag16" (bf16 modes);
+      // (2 was the Winograd packing, removed with its kernel)
       for (int dg = 0; dg < 4; ++dg) {
+        if (dg == 0 && mode != sdp::MODE_F32) continue;
         if (dg == 1 && !train_packs) continue;
-        if (dg == 2 && (s[2] != 3 || mode == sdp::MODE_F32)) continue;
+        if (dg == 2) continue;
         if (dg == 3 && mode == sdp::MODE_F32) continue;
-        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 1 ? "#dfrag" : dg == 2 ? "#wfrag" : "#frag16");
-        const int nt = dg == 2 ? 12 : (int)(s[2] * s[3]);
+        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 1 ? "#dfrag" : "#frag16");
+        const int nt = (int)(s[2] * s[3]);
         const size_t n = (size_t)s[0] * s[1] * nt;
         if (!dev.count(fk)) {
           void* p = nullptr;

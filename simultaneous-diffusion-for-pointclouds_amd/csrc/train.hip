@@ -97,9 +97,8 @@ struct TrainPlan {
     if (dry) return;
     ConvArgs a{};
     a.in = in.p;
-    a.wf = reinterpret_cast<const uint4*>(P(wkey + ".weight#frag"));
-    a.wfw = net->wino_w(wkey);
-    a.wf16 = getenv("SDP_FRAG16") && atoi(getenv("SDP_FRAG16")) == 0 ? nullptr : net->frag16_w(wkey);
+    a.wf = net->mode == MODE_F32 ? reinterpret_cast<const uint4*>(P(wkey + ".weight#frag")) : nullptr;
+    a.wf16 = net->mode == MODE_F32 ? nullptr : reinterpret_cast<const uint4*>(P(wkey + ".weight#frag16"));
     a.bias = o.bias ? P(wkey + ".bias") : nullptr;
     a.out = out.p;
     a.res = o.res;

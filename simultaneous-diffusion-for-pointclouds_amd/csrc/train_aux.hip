@@ -81,36 +81,6 @@ SDP_DEV uint32_t pack_slot16(const float* __restrict__ w, int Cout, int Cin, int
   return pk;
 }
 
-// Winograd F(2,3)-along-W packing consumed by wino_conv_kernel (wino_kernel.h), 32x32x16 fragments
-// over 12 transformed taps, tap = 4 kh + j, of U_j[kh] = (g0, (g0+g1+g2)/2, (g0-g1+g2)/2, g2)[j] over
-// the kernel row g = w[co][ci][kh][0..2]:
-//   [chunk = Cin/32][tap 12][nb = Cout/32][q = 2 s + hl, 4][lane 64][4 words: 8 bf16]
-// lane l holds Cout nb*32 + l%32, channels chunk*32 + 16 s + 8 (l/32) + 0..7 (hl: hi / lo part), so
-// each 16-B-per-lane fragment load of a wave reads 1 KiB contiguous
-SDP_DEV uint32_t pack_slot_wino(const float* __restrict__ w, int Cout, int Cin, int mode, size_t i) {
-  const int NB = Cout / 32;
-  const int word = i & 3;
-  const int lane = (i >> 2) & 63;
-  const int q = (i >> 8) & 3;
-  size_t r = i >> 10;
-  const int nb = r % NB;
-  r /= NB;
-  const int tap = r % 12;
-  const int ch = r / 12;
-  const int s = q >> 1, hl = q & 1, j0 = word * 2;
-  const int co = nb * 32 + (lane & 31), kh = tap >> 2, j = tap & 3;
-  uint32_t pk = 0;
-  for (int e = 0; e < 2; ++e) {
-    const int ci = ch * 32 + 16 * s + 8 * (lane >> 5) + j0 + e;
-    const float* g = w + ((size_t)co * Cin + ci) * 9 + kh * 3;
-    const float u = j == 0 ? g[0] : j == 3 ? g[2] : j == 1 ? 0.5f * ((g[0] + g[1]) + g[2]) : 0.5f * ((g[0] - g[1]) + g[2]);
-    const __bf16 hi = (__bf16)u;
-    const __bf16 q = (hl && mode == MODE_F32X3) ? (__bf16)(u - (float)hi) : hi;
-    pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
-  }
-  return pk;
-}
-
 __global__ void pack_weights_kernel(const float* __restrict__ w, uint32_t* __restrict__ out, int Cout, int Cin, int NT,
                                     int mode, int dgrad) {
   const size_t n = (size_t)Cout * Cin * NT;    // output 32-bit slots
@@ -124,9 +94,8 @@ __global__ void pack_weights_multi_kernel(const PackDesc* __restrict__ d, int mo
   const PackDesc e = d[blockIdx.y];
   const size_t n = (size_t)e.Cout * e.Cin * e.NT;
   for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x)
-    e.out[j] = e.dgrad == 2   ? pack_slot_wino(e.w, e.Cout, e.Cin, mode, j)
-               : e.dgrad == 3 ? pack_slot16(e.w, e.Cout, e.Cin, e.NT, mode, j)
-                              : pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
+    e.out[j] = e.dgrad == 3 ? pack_slot16(e.w, e.Cout, e.Cin, e.NT, mode, j)
+                            : pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
 }
 
 hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st) {

@@ -47,8 +47,10 @@ struct WgTile {
   static constexpr int A_PLANE = NPIX * 64;             // [px][32 ci] bf16
 };
 
-// OCC: 1 = one workgroup per CU, next tile's loads in registers; 2 = two workgroups per CU taking
-// turns (chunked staging); 3 = one workgroup per CU with the next two tiles' loads in flight
+// OCC: 1 = one workgroup per CU, next tile's loads in registers (fp32x3); 2 = two workgroups per CU
+// taking turns, chunked staging (bf16: 134.4 image-steps/s in the bf16 training step against 119.2
+// for OCC 1 and for one workgroup per CU with the next two tiles' loads in flight,
+// profiles/experiments/r03_train_ring_wgrad_ab.log)
 template <int MODE, int TC, int KS, int OCC>
 __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -74,12 +76,9 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
   });
 
-  // OCC 3: one workgroup per CU (512-register waves) with the global loads of the next TWO tiles in
-  // flight in two register sets, so a tile's load latency hides behind two tiles of MFMAs
-  constexpr int NSET = OCC == 3 ? 2 : 1;
-  float4 rdS[NSET][T::NUD], raS[NSET][T::NUA];
+  static_assert(OCC == 1 || OCC == 2, "OCC: 1 or 2");
+  float4 rdS[1][T::NUD], raS[1][T::NUA];
   int tb = 0, tph_r = 0, tph_c = 0, tsr0 = 0, tsc0 = 0;
-  int stb[NSET], ssr0[NSET], ssc0[NSET];   // the tile held by each register set (image, patch origin)
   auto decode = [&](int t) {
     tb = t / tiles_img;
     int r = t - tb * tiles_img;
@@ -192,7 +191,7 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
   auto store_a = [&](auto kb_, auto ke_, auto set_) {
     constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
     const float4* ra = raS[SET];
-    const int sb = OCC == 3 ? stb[SET] : tb, sr0_ = OCC == 3 ? ssr0[SET] : tsr0, sc0_ = OCC == 3 ? ssc0[SET] : tsc0;
+    const int sb = tb, sr0_ = tsr0, sc0_ = tsc0;
     const float* ssb = a.pro_ss + (size_t)sb * a.ss_bstride + ci0 * 2;
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
@@ -214,7 +213,6 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     }
   };
   using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
   using IND = std::integral_constant<int, T::NUD>;
   using INA = std::integral_constant<int, T::NUA>;
   // OCC 2: two workgroups per CU take turns (one stages while the other's MFMAs run), so a
@@ -277,34 +275,7 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       });
     }
   };
-  // OCC 3: load tile tt into register set SET (and remember its coordinates for the LDS store)
-  auto fetch_set = [&](auto set_, int tt) __attribute__((always_inline)) {
-    constexpr int SET = decltype(set_)::value;
-    decode(tt);
-    prep_tile();
-    stb[SET] = tb;
-    ssr0[SET] = tsr0;
-    ssc0[SET] = tsc0;
-    load_dy(I0{}, IND{}, set_);
-    load_a(I0{}, INA{}, set_);
-  };
-  auto step3 = [&](auto set_, int t) __attribute__((always_inline)) {
-    __syncthreads();   // the previous tile's MFMAs are done with the LDS tiles
-    store_dy(I0{}, IND{}, set_);
-    store_a(I0{}, INA{}, set_);
-    __syncthreads();
-    if (t + 2 < t_end) fetch_set(set_, t + 2);
-    compute();
-  };
-
-  if constexpr (OCC == 3) {
-    if (t_begin < t_end) fetch_set(I0{}, t_begin);
-    if (t_begin + 1 < t_end) fetch_set(I1{}, t_begin + 1);
-    for (int t = t_begin; t < t_end; t += 2) {
-      step3(I0{}, t);
-      if (t + 1 < t_end) step3(I1{}, t + 1);
-    }
-  } else {
+  {
     if (OCC == 1 && t_begin < t_end) {
       decode(t_begin);
       prep_tile();
@@ -391,27 +362,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __r
   *o = accumulate ? *o + s : s;
 }
 
-// staging scheme of the bf16 weight gradient (A/B knob SDP_WGRAD_OCC = 2 | 3 | 1; fp32x3 runs OCC 1).
-// Two workgroups per CU (2) beat one with the next two tiles' loads in flight (3) and one with the
-// next tile's (1): 134.4 vs 119.2 vs 119.2 image-steps/s in the bf16 training step
-// (profiles/experiments/r03_train_ring_wgrad_ab.log)
-static int wgrad_occ_bf16() {
-  static const int o = [] {
-    const char* e = getenv("SDP_WGRAD_OCC");
-    return e ? atoi(e) : 2;
-  }();
-  return o;
-}
-
 int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks) {
   const int tc = ((W / d) % 64 == 0) ? 64 : 32;
   const int total = B * (H / d) * (W / d) / 128 * d * d;
   (void)tc;
   const int blocks = (Cin / 32) * (Cout / 128);
-  // (the one-workgroup-per-CU scheme of the bf16 weight gradient aims at one round of 256; the
-  // split count also sizes the partial buffer, so it depends only on this process-wide knob)
-  const int target = wgrad_occ_bf16() == 3 ? WGRAD_TARGET_BLOCKS / 2 : WGRAD_TARGET_BLOCKS;
-  int S = (target + blocks - 1) / blocks;
+  int S = (WGRAD_TARGET_BLOCKS + blocks - 1) / blocks;
   S = S < total ? S : total;
   return S < 1 ? 1 : S;
 }
@@ -429,12 +385,7 @@ static hipError_t wgrad_occ(const WgradArgs& a, int ks, int tc, dim3 grid, hipSt
 template <int MODE>
 static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
   dim3 grid(S, a.Cin / 32, a.Cout / 128);
-  if constexpr (MODE == MODE_BF16) {
-    if (wgrad_occ_bf16() == 3) return wgrad_occ<MODE, 3>(a, ks, tc, grid, st);
-    if (wgrad_occ_bf16() == 1) return wgrad_occ<MODE, 1>(a, ks, tc, grid, st);
-    return wgrad_occ<MODE, 2>(a, ks, tc, grid, st);
-  }
-  return wgrad_occ<MODE, 1>(a, ks, tc, grid, st);
+  return wgrad_occ<MODE, MODE == MODE_BF16 ? 2 : 1>(a, ks, tc, grid, st);
 }
 
 hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,

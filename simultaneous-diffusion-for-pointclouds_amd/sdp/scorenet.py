@@ -121,8 +121,8 @@ class ScoreNet:
                                                        ws.data_ptr(), ws.numel(), _lib.stream()), "net_forward_langevin")
 
     def set_split(self, ways: int):
-        """Run each forward as `ways` part-batch forwards on as many streams (0 = default: env
-        SDP_SPLIT, else 2; 1 = off).  Results are identical; only the launch schedule changes."""
+        """Run each forward as `ways` part-batch forwards on as many streams (0 = the default, 2;
+        1 = off).  Results are identical; only the launch schedule changes."""
         _lib.check(_lib.lib().sdp_net_set_split(self._h, int(ways)), "set_split")
         self._ws.clear()                    # the workspace size depends on it
 

@@ -363,3 +363,25 @@ def test_kitti_sampler_end_to_end_matches_golden(net256):
     assert len(images) == 3
     for got, want in ((images[0].numpy(), f["new"]), (images[1].numpy(), f["new2"]), (images[2].numpy(), f["final"])):
         assert _close_frac(got, want, rtol=1e-4, atol=1e-4 * np.abs(want).max()) <= 1e-3
+
+
+@pytest.mark.parametrize("setting,min_step", [(5, 0), (7, 1)])
+def test_allforone_sampler_end_to_end_matches_golden(net256, setting, min_step):
+    """AllForOne loop (models/__init__.py:112-602) vs the reference-generated golden: the setting-5
+    cc ramp over L=3 levels, the level-0 shared images, denoise + final consistency."""
+    from oracle.gen_golden import CIRCLE_MODS
+    from sdp.sampling import anneal_Langevin_dynamics_inpainting_simultaneous_basic as samp
+    from sdp.weights import get_sigmas_np
+    tag = f"a_e2e_set{setting}"
+    f = _g(f"allforone_e2e_set{setting}_b3_64x256.npz")
+    case = GI.merge_case(tag, 3, 64, 256)
+    x0 = torch.from_numpy(GI.scorenet_input(tag, 3, 64, 256)).to(DEV)
+    t = lambda a: torch.from_numpy(a).to(DEV)
+    images, _, shared = samp(x0, t(case["ref"]), t(case["mask"]), t(case["sky"]), None, min_step, setting, net256,
+                             get_sigmas_np()[229:232], torch.tensor(CIRCLE_MODS[:3]), 3, n_steps_each=2,
+                             step_lr=6.2e-6, existMask=t(case["exist"]), denoise=True, verbose=False, grad_ref=1,
+                             correlation_coefficient=0.01, noise_fn=_noise_feed(tag))
+    assert len(images) == 3 and len(shared) == (2 if min_step == 0 else 0)
+    for got, k in zip(images + shared, ("new", "new2", "final", "shared0", "shared1")):
+        want = f[k]
+        assert _close_frac(got.numpy(), want, rtol=1e-4, atol=1e-4 * np.abs(want).max()) <= 1e-3, k

@@ -199,6 +199,24 @@ def test_kitti_sampler_end_to_end(params128):
     np.testing.assert_allclose(images[2], f["final"], rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("setting,min_step", [(5, 0), (7, 1)])
+def test_allforone_sampler_end_to_end(params128, setting, min_step):
+    """oracle sampler_allforone == the reference AllForOne loop (models/__init__.py:112-602):
+    the setting-5 cc ramp at L=3, the level-0 shared images, denoise and final consistency."""
+    from oracle.gen_golden import CIRCLE_MODS
+    tag = f"a_e2e_set{setting}"
+    f = _g(f"allforone_e2e_set{setting}_b3_64x256.npz")
+    case = GI.merge_case(tag, 3, 64, 256)
+    x0 = GI.scorenet_input(tag, 3, 64, 256)
+    images, _, shared = S.sampler_allforone(x0, case["ref"], case["mask"], case["sky"], min_step, setting,
+                                            _score_fn(params128), get_sigmas_np()[229:232], np.array(CIRCLE_MODS[:3]),
+                                            3, 2, 6.2e-6, case["exist"], _noise_feed(tag))
+    assert len(images) == 3 and len(shared) == (2 if min_step == 0 else 0)
+    assert (f["new"] != 0).mean() > 0.3          # the merge populated the views
+    for got, k in zip(images + shared, ("new", "new2", "final", "shared0", "shared1")):
+        np.testing.assert_allclose(got, f[k], rtol=1e-5, atol=1e-5, err_msg=k)
+
+
 def dsm_case(H, W, B, tag="dsm"):
     """Inputs of oracle/gen_golden.py gen_dsm (same generator stream)."""
     r = GI.rng(tag)

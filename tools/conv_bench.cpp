@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
   sdp::ConvArgs a{};
   a.in = in; a.wf = reinterpret_cast<const uint4*>(wf);
   // the library's forward reads the coalesced 16x16 packing (#frag16); random words fit any layout
-  if (!(getenv("SDP_FRAG16") && atoi(getenv("SDP_FRAG16")) == 0)) a.wf16 = a.wf; a.bias = bias; a.out = out; a.pro_ss = ss;
+  a.wf16 = a.wf; a.bias = bias; a.out = out; a.pro_ss = ss;
   a.ss_bstride = 2 * Cin; a.stats = stats; a.B = B; a.H = H; a.W = W; a.Cin = Cin; a.Cout = Cout;
   a.dil = dil; a.circular = 1; a.pro_mode = sdp::PRO_AFFINE_ELU; a.epi_elu = 0;
   unsigned long long* dbg;
