@@ -19,6 +19,7 @@
  *   sdp_net_forward_train  scores = scorenet(perturbed, labels) in train mode   losses/dsm.py:85
  *   sdp_dsm_loss           anneal_dsm_score_estimation_with_mask            losses/dsm.py:67-119
  *   sdp_net_backward       loss.backward()                                  runners/ncsn_runner_kitti_simultaneous.py:230
+ *   sdp_net_backward_buckets  loss.backward() + DataParallel's gradient reduce  (kitti runner :104,481,230)
  *   sdp_adam_ema_step      optimizer.step() (Adam, losses/__init__.py:10-20) + EMAHelper.update (models/ema.py:16-21)
  *   sdp_optim_ema_step     optimizer.step() of Adam / RMSprop / SGD (get_optimizer, losses/__init__.py:3-13) + EMA
  *   sdp_range_project      point_cloud_to_range_image                       datasets/lidar_utils.py:54-347
@@ -104,8 +105,9 @@ int sdp_net_profile_enable(sdp_net* net, int enable);
 int sdp_net_profile_read(sdp_net* net, char* buf, size_t cap, int* n_launches);
 
 /* ---- parameters as one device arena (training) ------------------------------------------
- * Every learnable parameter (state_dict keys minus the "sigmas" buffer), float32, in key order,
- * each at a 64-float aligned offset.  sdp_net_bind_params copies the current values into a
+ * Every learnable parameter (state_dict keys minus the "sigmas" buffer), float32, each at a
+ * 64-float aligned offset, in the order sdp_net_backward finishes their gradients (head first,
+ * begin_conv last; sdp_net_param_info enumerates it).  sdp_net_bind_params copies the current values into a
  * caller-owned device arena of sdp_net_param_arena_floats floats and makes it the net's
  * parameter storage; after the caller changes it (optimizer), sdp_net_repack rebuilds the
  * packed conv weights on `stream`.  Gradient arenas use the same layout.                    */
@@ -125,6 +127,15 @@ int sdp_net_forward_train(sdp_net* net, const float* x, const int64_t* labels, f
                           void* workspace, size_t workspace_bytes, void* stream);
 int sdp_net_backward(sdp_net* net, const float* dscore, int B, void* workspace, size_t workspace_bytes,
                      float* grads, void* stream);
+/* sdp_net_backward with gradient buckets for a data-parallel reduce overlapped with the backward
+ * (replaces the implicit gradient reduce of torch.nn.DataParallel,
+ * runners/ncsn_runner_kitti_simultaneous.py:104,481): bucket i is the arena range
+ * [bucket_end[i-1], bucket_end[i]) (floats, increasing, <= sdp_net_param_arena_floats); events[i]
+ * (hipEvent_t) is recorded on `stream` as soon as the launches that finish every gradient of that
+ * range are enqueued, so a communication stream can wait on it while the backward goes on. */
+int sdp_net_backward_buckets(sdp_net* net, const float* dscore, int B, void* workspace, size_t workspace_bytes,
+                             float* grads, int n_buckets, const size_t* bucket_end, void* const* events,
+                             void* stream);
 /* loss = mean_b 1/2 * sum_i (mask*(score - target))^2 * n_img / sum(mask) * sigma_b^p with
  * target = -noise / sigma_b^2 (noise already scaled by sigma_b, as the reference passes it);
  * writes dscore = d loss / d score, loss[0], loss_per[b] (optional).  mask float32 0/1,

@@ -41,7 +41,7 @@ static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int 
 //       4 x 32 / 2 x 64 tiles, profiles/experiments/r02_tile_width_ab.log);
 //     128-channel outputs: 128 px x 128 Cout, 8 x 16 tiles, 2 waves, two workgroups per CU (one's
 //       prologue and epilogue run under the other's MFMAs: 214.5 -> 211.0 us per 128->128 @64x1024
-//       launch against 256 px x 128 Cout on 4 waves, profiles/experiments/r03_half_ab.log);
+//       launch against 256 px x 128 Cout on 4 waves, profiles/experiments/r03_half_wg_128only.log);
 //   exact fp32 (32x32 MFMAs, 32-pixel fragment rows): 4 x 32 tiles (2 x 64 where the sub-grid needs
 //     it) of 128 px x 256 Cout, or 8 x 32 tiles of 256 px x 128 Cout;
 //   pooled (ConvMeanPool) and 1x1 layers: 2 x 64 tiles of 128 px x 256 Cout.

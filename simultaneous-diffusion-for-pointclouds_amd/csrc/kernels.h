@@ -35,6 +35,7 @@ struct PackDesc {
 };
 hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st);
 hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k, int mode, int dgrad, hipStream_t st);
+// InstanceNorm++ backward: C a power of two in [32, 512], HW a multiple of 512 (else hipErrorInvalidValue)
 hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
                          int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
                          float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st);

@@ -444,13 +444,26 @@ int sdp_net_finalize(sdp_net* net) {
       chk(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice), "hipMemcpy");
       net->dev[k] = d;
     };
-    // every learnable parameter in one arena, [key order][64-float aligned] (sdp_net_param_info)
+    // every learnable parameter in one arena, 64-float aligned (sdp_net_param_info), in the order
+    // the backward finishes their gradients (train.hip grad_completion_order; the parameters it
+    // does not name, in key order after them): gradient buckets are then contiguous arena ranges
     net->layout.clear();
     size_t off = 0;
-    for (auto& kv : net->host) {
-      if (kv.first == "sigmas") continue;
-      net->layout.push_back({kv.first, off, kv.second.data.size()});
-      off += (kv.second.data.size() + 63) / 64 * 64;
+    std::vector<std::string> order;
+    try {
+      order = grad_completion_order(net);
+    } catch (const std::exception&) {   // an incomplete parameter set: key order (its forward fails anyway)
+      order.clear();
+    }
+    std::map<std::string, bool> placed;
+    for (auto& kv : net->host)
+      if (kv.first != "sigmas") order.push_back(kv.first);   // (duplicates skipped below)
+    for (const auto& k : order) {
+      auto it = net->host.find(k);
+      if (it == net->host.end() || k == "sigmas" || placed[k]) continue;
+      placed[k] = true;
+      net->layout.push_back({k, off, it->second.data.size()});
+      off += (it->second.data.size() + 63) / 64 * 64;
     }
     net->arena_floats = off;
     chk(hipMalloc(&net->arena, off * 4), "hipMalloc");

@@ -167,3 +167,7 @@ struct sdp_net {
 };
 
 int sdp_fail(const std::string& m);
+
+namespace sdp {
+std::vector<std::string> grad_completion_order(sdp_net* net);   // train.hip
+}

@@ -45,6 +45,14 @@ struct TrainPlan {
   float *wpart = nullptr, *bpart = nullptr, *spart = nullptr, *coef = nullptr, *ppart = nullptr, *epart = nullptr;
   size_t wpart_n = 0;
   float* grads = nullptr;
+  // gradient completion: the parameters whose gradient each producer finishes, in backward order
+  // (grad_order, recorded by every run, dry or not); with bucket events, events[i] is recorded on
+  // the stream once the finished parameters cover the arena prefix [0, bucket_end[i])
+  std::vector<std::string> grad_order;
+  int n_buckets = 0, next_bucket = 0;
+  const size_t* bucket_end = nullptr;
+  hipEvent_t const* bucket_ev = nullptr;
+  size_t done_prefix = 0;             // floats of the arena prefix whose gradients are final
   size_t fwd_bytes = 0;
   size_t ws_need = 0;                 // forward + backward bytes (dry run), 0 = unknown
 
@@ -75,6 +83,18 @@ struct TrainPlan {
     return it->second;
   }
   int ks_of(const std::string& wkey) const { return (int)net->host.at(wkey + ".weight").shape[2]; }
+  // the gradients of `keys` are final once the launches enqueued so far have run
+  void finished(std::initializer_list<std::string> keys) {
+    for (const auto& k : keys) {
+      grad_order.push_back(k);
+      if (dry || !n_buckets) continue;
+      for (const auto& e : net->layout)
+        if (e.key == k) done_prefix = std::max(done_prefix, e.offset + (e.numel + 63) / 64 * 64);
+    }
+    if (dry) return;
+    while (next_bucket < n_buckets && done_prefix >= bucket_end[next_bucket])
+      ok(hipEventRecord(bucket_ev[next_bucket++], st), "hipEventRecord (gradient bucket)");
+  }
 
   // ------------------------------------------------------------------ forward pieces
   struct Opt {
@@ -296,7 +316,12 @@ struct TrainPlan {
   // ------------------------------------------------------------------ backward pieces
   void wgrad(const std::string& k, const T4& in, int pro, const float* ss, const T4& dy, int dil, bool circular, int ks,
              bool with_bias) {
-    if (dry) return;
+    if (!dry) wgrad_launch(k, in, pro, ss, dy, dil, circular, ks, with_bias);
+    if (with_bias) finished({k + ".weight", k + ".bias"});
+    else finished({k + ".weight"});
+  }
+  void wgrad_launch(const std::string& k, const T4& in, int pro, const float* ss, const T4& dy, int dil, bool circular,
+                    int ks, bool with_bias) {
     WgradArgs a{};
     a.in = in.p;
     a.pro_ss = pro == PRO_AFFINE_ELU ? ss : P("#ident_ss");
@@ -341,10 +366,11 @@ struct TrainPlan {
     ok(conv_dgrad(net->mode, a, ks, st, &why), std::string(why) + " (" + k + ")");
   }
   void inpp_back(const std::string& nkey, const T4& g, const T4& h, const float* r1, const float* r2, const T4& out) {
-    if (dry) return;
-    ok(inpp_backward(g.p, h.p, F(nkey + "#nst"), P(nkey + ".alpha"), P(nkey + ".gamma"), B, h.H * h.W, h.C, spart, coef,
-                     ppart, G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st),
-       "inpp_backward " + nkey);
+    if (!dry)
+      ok(inpp_backward(g.p, h.p, F(nkey + "#nst"), P(nkey + ".alpha"), P(nkey + ".gamma"), B, h.H * h.W, h.C, spart,
+                       coef, ppart, G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st),
+         "inpp_backward " + nkey);
+    finished({nkey + ".alpha", nkey + ".gamma", nkey + ".beta"});
   }
 
   T4 resb(const std::string& k, const T4& dout, bool down, int dil, const float* extra) {
@@ -441,6 +467,9 @@ struct TrainPlan {
   void backward(const float* dscore, float* grad_arena) {
     used = fwd_bytes;
     grads = grad_arena;
+    grad_order.clear();
+    next_bucket = 0;
+    done_prefix = 0;
     // scratch (upper bounds over every layer of the network)
     wpart_n = (size_t)(WGRAD_TARGET_BLOCKS + 64) * 9 * 128 * 32;   // >= splits x 9 x Cin x Cout for every conv
     wpart = take(wpart_n);
@@ -458,6 +487,7 @@ struct TrainPlan {
       ok(end_conv_backward(dscore, P("sigmas"), lab, P("end_conv.weight"), o.p, F("normalizer#ss"), g.p, epart,
                            G("end_conv.weight"), G("end_conv.bias"), B, H, W, st),
          "end_conv_backward");
+    finished({"end_conv.weight", "end_conv.bias"});
     T4 d_o = like(o);
     inpp_back("normalizer", g, o, nullptr, nullptr, d_o);
     auto r4 = refineb("refine4", d_o, true, 3);      // -> d L1 (part), d ref3
@@ -475,10 +505,30 @@ struct TrainPlan {
     if (!dry)
       ok(begin_conv_wgrad(xin, d.p, epart, G("begin_conv.weight"), G("begin_conv.bias"), B, H, W, st),
          "begin_conv_wgrad");
+    finished({"begin_conv.weight", "begin_conv.bias"});
+    done_prefix = net->arena_floats;   // every gradient is final: the remaining buckets complete here
+    finished({});
   }
 };
 
 void destroy_plan(TrainPlan* p) { delete p; }
+
+// The parameters in the order the backward finishes their gradients (a dry run of the plan: host
+// bookkeeping only).  sdp_net_finalize lays the parameter arena out in this order, so the arena
+// prefix whose gradients are final grows monotonically during sdp_net_backward -- the gradient
+// buckets of sdp_net_backward_buckets are contiguous ranges that complete one after another.
+std::vector<std::string> grad_completion_order(sdp_net* net) {
+  TrainPlan p;
+  p.net = net;
+  p.B = 1;
+  p.H = net->d.H;
+  p.W = net->d.W;
+  p.C = net->d.ngf;
+  p.dry = true;
+  p.forward(nullptr, nullptr, nullptr);
+  p.backward(nullptr, nullptr);
+  return p.grad_order;
+}
 
 static TrainPlan* plan_for(sdp_net* net, int B) {
   if (net->plan && net->plan->B == B) return net->plan;
@@ -563,6 +613,31 @@ int sdp_net_backward(sdp_net* net, const float* dscore, int B, void* ws, size_t 
     p->backward(dscore, grads);
   } catch (const std::exception& e) {
     return tfail(std::string("sdp_net_backward: ") + e.what());
+  }
+  return 0;
+}
+
+int sdp_net_backward_buckets(sdp_net* net, const float* dscore, int B, void* ws, size_t ws_bytes, float* grads,
+                             int n_buckets, const size_t* bucket_end, void* const* events, void* stream) {
+  if (!net || !dscore || !ws || !grads || B <= 0 || n_buckets < 0 || (n_buckets && (!bucket_end || !events)))
+    return tfail("sdp_net_backward_buckets: bad argument");
+  for (int i = 0; i < n_buckets; ++i)
+    if (!events[i] || (i && bucket_end[i] <= bucket_end[i - 1]) || bucket_end[i] > net->arena_floats)
+      return tfail("sdp_net_backward_buckets: bucket ends must increase within the arena, events non-null");
+  TrainPlan* p = net->plan;
+  if (!p || p->dry || p->B != B || p->base != ws || p->saved.empty())
+    return tfail("sdp_net_backward_buckets: no tape -- call sdp_net_forward_train with this workspace and batch first");
+  try {
+    p->st = reinterpret_cast<hipStream_t>(stream);
+    p->cap = ws_bytes;
+    p->n_buckets = n_buckets;
+    p->bucket_end = bucket_end;
+    p->bucket_ev = reinterpret_cast<hipEvent_t const*>(events);
+    p->backward(dscore, grads);
+    p->n_buckets = 0;
+  } catch (const std::exception& e) {
+    p->n_buckets = 0;
+    return tfail(std::string("sdp_net_backward_buckets: ") + e.what());
   }
   return 0;
 }

@@ -278,6 +278,10 @@ __global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __rest
 
 static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 256 * 32); }
 
+// Channel range: C a power of two in [32, 512] (the network's norms are 128 and 256 wide): the reduce
+// block's 1024 threads hold C/4 channel groups x 4096/C pixel lanes, C/4 must divide 256 (the apply
+// kernel's channel-fixed stride) and each lane's share of a 512-pixel group a multiple of 4
+// (C % 32 == 0); anything else returns hipErrorInvalidValue (kernels.h).
 hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
                          int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
                          float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st) {

@@ -54,7 +54,8 @@ def parse_args_and_config(argv=None):
     p.add_argument("--ckpt", type=str, default=None, help="LiDARGen checkpoint (list format with EMA shadow)")
     p.add_argument("--precision", type=str, default="fp32x3", choices=["fp32x3", "fp32", "bf16"])
     p.add_argument("--num_batches", type=int, default=None,
-                   help="sampling: batches to sample (default 1); training: batches per epoch "
+                   help="sampling: batches to sample (default 1; scene completion: 0 or -1 = the whole "
+                        "validation split); training: batches per epoch "
                         "(default: the training split's length // global batch, 1 for the procedural source)")
     p.add_argument("--n_iters", type=int, default=None)
     p.add_argument("--snapshot_freq", type=int, default=None)

@@ -60,6 +60,7 @@ _SIGS = {
     "sdp_net_train_workspace_size": (I, [P, I, C.POINTER(SZ)]),
     "sdp_net_forward_train": (I, [P, P, P, P, I, P, SZ, P]),
     "sdp_net_backward": (I, [P, P, I, P, SZ, P, P]),
+    "sdp_net_backward_buckets": (I, [P, P, I, P, SZ, P, I, C.POINTER(SZ), C.POINTER(P), P]),
     "sdp_dsm_loss": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
     "sdp_adam_ema_step": (I, [P, P, P, P, P, SZ, F, F, F, F, I, F, P]),
     "sdp_optim_ema_step": (I, [I, P, P, P, P, P, P, SZ, F, F, F, F, F, I, F, P]),

@@ -329,7 +329,9 @@ class Runner:
         folder = self.args.image_folder
         ck = c.sampling.ckpt_id
         fetch, n_val = self._completion_source(B, aB, H, W)
-        n_batches = min(getattr(self.args, "num_batches", None) or 1, n_val)
+        nb = getattr(self.args, "num_batches", None)
+        # --num_batches 0 (or -1) = the whole validation split, as the reference iterates its dataloader
+        n_batches = n_val if nb is not None and nb <= 0 else min(nb or 1, n_val)
         time_taken = np.zeros(max(n_val, 2)) + 999999
         writer = rank == 0
         n_mega = B // aB
@@ -416,8 +418,10 @@ class Runner:
         """Test batches of the every-100-steps EMA evaluation (kitti:84-95, 247-251): the test split
         of the dataset (``get_dataset``'s second return) through its own MySampler iterator, never
         the training iterator.  Only rank 0 evaluates, so the draws (the sampler shuffles and every
-        item's roll come from the global np.random stream) run on a saved-and-restored np.random
-        state: the ranks' training streams stay in lockstep and their global-batch slices disjoint."""
+        item's roll come from the global np.random stream) run on an np.random state of their own
+        (seeded once, carried from evaluation to evaluation) swapped in around each draw: the ranks'
+        training streams stay in lockstep, their global-batch slices disjoint, and the evaluation
+        never re-draws the numbers the next training batch will draw."""
         c = self.config
         H, W = c.data.image_size, c.data.image_width
         root = getattr(self.args, "kitti_root", None)
@@ -431,10 +435,12 @@ class Runner:
             return synth
         dset = kitti360.get_dataset(c.data.dataset, None, c, split="test", root=root, device=self.device)
         n_batches = max(1, len(dset) // Bt)
-        state = {"it": None}
+        eval_seed = (getattr(self.args, "seed", 1234) * 1000003 + 0x5EED) % (2 ** 32)
+        state = {"it": None, "rng": np.random.RandomState(eval_seed).get_state()}
 
         def fetch(i):
             saved = np.random.get_state()
+            np.random.set_state(state["rng"])
             try:
                 items = []
                 for _ in range(Bt):
@@ -447,6 +453,7 @@ class Runner:
                         items.append(next(state["it"]))
                 b = kitti360.collate([dset[j] for j in items])
             finally:
+                state["rng"] = np.random.get_state()
                 np.random.set_state(saved)
             return b[0], b[1], b[2]
         return fetch

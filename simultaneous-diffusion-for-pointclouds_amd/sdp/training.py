@@ -13,8 +13,10 @@ Mirrors the reference's training interface:
   * ``train_step`` -- one inner-loop iteration of the kitti runner's ``train()``
     (runners/ncsn_runner_kitti_simultaneous.py:186-235).
 
-Data-parallel training: one process per GPU, gradients averaged with one RCCL all-reduce of
-the flat gradient arena (``dist_group``), the DDP equivalent of the reference's DataParallel.
+Data-parallel training: one process per GPU; the flat gradient arena is averaged over the ranks
+of ``dist_group`` in buckets whose RCCL all-reduces overlap the backward (sdp/gradreduce.py;
+bf16 on the wire for bf16 training, the fp32 arena stays the master copy) -- the DDP equivalent of
+the reference's DataParallel.
 """
 from __future__ import annotations
 
@@ -38,7 +40,7 @@ class Trainer:
     def __init__(self, net: ScoreNet, lr: float = 1e-4, beta1: float = 0.9, beta2: float = 0.999,
                  eps: float = 1e-8, ema: bool = True, ema_mu: float = 0.999, device="cuda", dist_group=None,
                  optimizer: str = "Adam", weight_decay: float = 0.0, amsgrad: bool = False,
-                 alpha: float = 0.99, momentum: float = 0.9):
+                 alpha: float = 0.99, momentum: float = 0.9, grad_wire_dtype=None, bucket_floats=None):
         if net.precision not in ("fp32x3", "bf16"):
             raise ValueError("training runs in precision fp32x3 or bf16")
         if optimizer not in self.OPTIMIZERS:
@@ -50,6 +52,10 @@ class Trainer:
         self.weight_decay, self.amsgrad, self.alpha, self.momentum = float(weight_decay), bool(amsgrad), alpha, momentum
         self.ema, self.ema_mu = ema, ema_mu
         self.dist_group = dist_group
+        # gradient all-reduce on the wire: bf16 for bf16 training (59.4 MB), fp32 for fp32x3
+        self.grad_wire_dtype = grad_wire_dtype or (torch.bfloat16 if net.precision == "bf16" else torch.float32)
+        self.bucket_floats = bucket_floats
+        self._reducer = None
         n = _lib.SZ()
         _lib.check(L.sdp_net_param_arena_floats(net._h, _lib.C.byref(n)), "param_arena_floats")
         cnt = _lib.I()
@@ -139,18 +145,33 @@ class Trainer:
     def zero_grad(self):
         self.grads.zero_()
 
+    def reducer(self):
+        """The bucketed gradient all-reduce over dist_group (sdp/gradreduce.py), built on first use."""
+        if self._reducer is None:
+            from .gradreduce import DEFAULT_BUCKET_FLOATS, BucketedGradReducer
+            self._reducer = BucketedGradReducer(self.grads, self.layout, self.dist_group,
+                                                self.bucket_floats or DEFAULT_BUCKET_FLOATS, self.grad_wire_dtype)
+        return self._reducer
+
     def backward(self, dscore: torch.Tensor | None = None):
-        """loss.backward(): gradient arena <- d loss / d parameters (averaged over ranks)."""
+        """loss.backward(): gradient arena <- d loss / d parameters (averaged over ranks, the
+        reduce of each bucket overlapping the rest of the backward)."""
         d = self._dscore if dscore is None else dscore.contiguous()
         if d is None or self._B is None:
             raise RuntimeError("Trainer.backward: run forward + dsm_loss first")
         ws = self._workspace(self._B)
-        _lib.check(self.L.sdp_net_backward(self.net._h, d.data_ptr(), self._B, ws.data_ptr(), ws.numel(),
-                                           self.grads.data_ptr(), _lib.stream()), "backward")
-        if self.dist_group is not None:
-            import torch.distributed as dist
-            dist.all_reduce(self.grads, op=dist.ReduceOp.SUM, group=self.dist_group)
-            self.grads.div_(dist.get_world_size(self.dist_group))
+        if self.dist_group is None:
+            _lib.check(self.L.sdp_net_backward(self.net._h, d.data_ptr(), self._B, ws.data_ptr(), ws.numel(),
+                                               self.grads.data_ptr(), _lib.stream()), "backward")
+            return
+        red = self.reducer()
+        n = len(red.ends)
+        ends = (_lib.SZ * n)(*red.ends)
+        evs = (_lib.P * n)(*red.event_handles())
+        _lib.check(self.L.sdp_net_backward_buckets(self.net._h, d.data_ptr(), self._B, ws.data_ptr(), ws.numel(),
+                                                   self.grads.data_ptr(), n, ends, evs, _lib.stream()),
+                   "backward_buckets")
+        red.reduce(self.grads)
 
     def step(self):
         """optimizer.step() + ema_helper.update(score), then re-pack the conv weights."""
@@ -171,14 +192,18 @@ class Trainer:
         _lib.check(self.L.sdp_net_repack(self.net._h, _lib.stream()), "repack")
 
     def optimizer_state_dict(self):
-        """optimizer.state_dict() in torch's format (per-parameter state keyed by index)."""
+        """optimizer.state_dict() in torch's format: per-parameter state keyed by the index of the
+        parameter in the module's parameters() order (NCSN_LiDAR_small registration order, the
+        order of sdp.weights.param_spec), independent of the device arena's layout."""
+        where = {k: (off, numel) for k, off, numel in self.layout}
         state = {}
-        for i, (k, off, numel) in enumerate(self.layout):
+        for i, k in enumerate(self.shapes):
+            off, numel = where[k]
             e = {n: t[off:off + numel].view(self.shapes[k]).cpu() for n, t in self.opt_state.items()}
             if self.optimizer != "SGD":
                 e["step"] = torch.tensor(float(self.steps))
             state[i] = e
-        group = {"lr": self.lr, "weight_decay": self.weight_decay, "params": list(range(len(self.layout)))}
+        group = {"lr": self.lr, "weight_decay": self.weight_decay, "params": list(range(len(self.shapes)))}
         if self.optimizer == "Adam":
             group.update(betas=(self.beta1, self.beta2), eps=self.eps, amsgrad=self.amsgrad)
         elif self.optimizer == "RMSProp":

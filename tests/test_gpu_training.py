@@ -159,14 +159,18 @@ def test_get_optimizer_kinds_match_torch(name):
     assert torch.allclose(tr.params.cpu(), ref_p.data, rtol=1e-6, atol=1e-7)
     assert torch.allclose(tr.shadow.cpu(), shadow, rtol=1e-6, atol=1e-7)
     # the state_dict in torch's format carries the same optimizer state
+    # (index i = the i-th parameter in module order, wherever the arena keeps it)
     sd = tr.optimizer_state_dict()
     ref_state = opt.state[ref_p]
-    for k, v in sd["state"][0].items():
-        if k == "step":
-            assert float(v) == float(ref_state["step"])
-        else:
-            n = v.numel()
-            assert torch.allclose(v.flatten(), ref_state[k].flatten()[:n], rtol=1e-5, atol=1e-7), k
+    where = {k: off for k, off, _ in tr.layout}
+    for i in (0, len(tr.shapes) - 1):
+        off = where[list(tr.shapes)[i]]
+        for k, v in sd["state"][i].items():
+            if k == "step":
+                assert float(v) == float(ref_state["step"])
+            else:
+                n = v.numel()
+                assert torch.allclose(v.flatten(), ref_state[k].flatten()[off:off + n], rtol=1e-5, atol=1e-7), k
 
 
 def test_get_optimizer_unknown_raises():
@@ -207,3 +211,76 @@ def test_train_step_runs_and_reduces_loss():
         losses.append(loss.item())
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0], losses
+
+
+def test_arena_in_gradient_completion_order_and_bucket_events(case):
+    """The parameter arena follows the order the backward finishes the gradients (head first,
+    begin_conv last), so sdp_net_backward_buckets can record each bucket's event as soon as the
+    bucket is final; the gradients equal sdp_net_backward's bit for bit."""
+    from sdp import _lib
+    from sdp.gradreduce import bucket_ends
+    net = ScoreNet(H=H, W=W, precision="fp32x3").load_synthetic()
+    tr = Trainer(net)
+    keys = [k for k, _, _ in tr.layout]
+    assert keys[0] == "end_conv.weight" and keys[-1] in ("begin_conv.weight", "begin_conv.bias")
+    assert [off for _, off, _ in tr.layout] == sorted(off for _, off, _ in tr.layout)
+    dev = "cuda"
+    anneal_dsm_score_estimation_with_mask(tr, case["X"].to(dev), case["used"].to(dev), case["noise"].to(dev),
+                                          case["mask"].to(dev), None, net.sigmas.to(dev), case["labels"].to(dev))
+    tr.backward()
+    ref = tr.grads.clone()
+    ends = bucket_ends(tr.layout, tr.grads.numel(), 4 << 20)
+    evs = [torch.cuda.Event() for _ in ends]
+    for e in evs:
+        e.record()
+    tr.grads.fill_(float("nan"))
+    ws = tr._workspace(tr._B)
+    n = len(ends)
+    main = torch.cuda.current_stream()
+    _lib.check(_lib.lib().sdp_net_backward_buckets(net._h, tr._dscore.data_ptr(), tr._B, ws.data_ptr(), ws.numel(),
+                                                   tr.grads.data_ptr(), n, (_lib.SZ * n)(*ends),
+                                                   (_lib.P * n)(*[e.cuda_event for e in evs]), _lib.stream()),
+               "backward_buckets")
+    # the bucket copies, taken on a side stream after each bucket's event only, see final gradients
+    side = torch.cuda.Stream()
+    snap = torch.empty_like(tr.grads)
+    a = 0
+    with torch.cuda.stream(side):
+        for b, e in zip(ends, evs):
+            side.wait_event(e)
+            snap[a:b].copy_(tr.grads[a:b])
+            a = b
+    main.wait_stream(side)
+    torch.cuda.synchronize()
+    assert len(ends) >= 3
+    assert torch.equal(tr.grads, ref)
+    assert torch.equal(snap, ref)
+
+
+def test_bucketed_reduce_rccl_world1_bf16_wire(case):
+    """The overlapped bucket all-reduce on RCCL (world size 1 on this one-GPU box): events, the
+    communication stream, the bf16 wire and the fp32 write-back -- the averaged arena equals the
+    single-process gradients rounded to bf16."""
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        net = ScoreNet(H=H, W=W, precision="bf16").load_synthetic()
+        tr = Trainer(net, dist_group=dist.group.WORLD, bucket_floats=4 << 20)
+        assert tr.grad_wire_dtype == torch.bfloat16
+        solo = Trainer(ScoreNet(H=H, W=W, precision="bf16").load_synthetic())
+        dev = "cuda"
+        for t in (tr, solo):
+            anneal_dsm_score_estimation_with_mask(t, case["X"].to(dev), case["used"].to(dev), case["noise"].to(dev),
+                                                  case["mask"].to(dev), None, t.net.sigmas.to(dev),
+                                                  case["labels"].to(dev))
+            t.backward()
+        torch.cuda.synchronize()
+        assert len(tr.reducer().ends) >= 3
+        assert torch.equal(tr.grads, solo.grads.to(torch.bfloat16).float())
+    finally:
+        dist.destroy_process_group()
