@@ -146,7 +146,7 @@ int sdp_dsm_loss(const float* score, const float* noise, const float* mask, cons
 /* torch.optim.Adam step (weight_decay 0, amsgrad off) over n floats, step = 1, 2, ...; then
  * ema_shadow = (1 - ema_mu)*p + ema_mu*ema_shadow if ema_shadow is not NULL.                 */
 int sdp_adam_ema_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema_shadow,
-                      size_t n, float lr, float beta1, float beta2, float eps, int step, float ema_mu,
+                      size_t n, double lr, double beta1, double beta2, double eps, int step, double ema_mu,
                       void* stream);
 /* optimizer.step() of every optimizer get_optimizer builds (losses/__init__.py:3-13), in torch's
  * per-element order, then the EMA update as above.  g <- g + weight_decay*p first (all kinds).
@@ -157,8 +157,10 @@ int sdp_adam_ema_step(float* params, const float* grads, float* exp_avg, float* 
  * step = 1, 2, ... (the optimizer's step count after this step).                            */
 enum sdp_optim_kind { SDP_OPTIM_ADAM = 0, SDP_OPTIM_RMSPROP = 1, SDP_OPTIM_SGD = 2 };
 int sdp_optim_ema_step(int kind, float* params, const float* grads, float* state0, float* state1, float* state2,
-                       float* ema_shadow, size_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
-                       int step, float ema_mu, void* stream);
+                       float* ema_shadow, size_t n, double lr, double beta1, double beta2, double eps,
+                       double weight_decay, int step, double ema_mu, void* stream);
+/* (hyperparameters are host doubles -- the Python floats torch.optim and EMAHelper compute with:
+ *  1 - beta, 1 - mu and the bias corrections are formed in double and rounded once)          */
 
 /* ---- Langevin update ------------------------------------------------------------------ *
  * x <- x + step*g' + grad_ref*lik + noise*noise_scale   (float32, reference evaluation order)

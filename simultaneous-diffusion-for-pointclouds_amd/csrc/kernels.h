@@ -60,6 +60,8 @@ struct OptimHyper {
   float step_size;       // Adam: lr / bias_correction1; RMSprop, SGD: lr
   float bc2_sqrt;        // Adam: sqrt(bias_correction2)
   float mu;              // EMA rate
+  float omb1, omb2, ommu; // 1 - b1, 1 - b2, 1 - mu: computed from the double hyperparameters and
+                         //   rounded once, as torch (Python float scalars) and EMAHelper do
   int first;             // SGD: first step (momentum buffer = g)
 };
 // s0, s1, s2: Adam exp_avg, exp_avg_sq, max_exp_avg_sq (amsgrad, else null); RMSprop square_avg; SGD momentum_buffer

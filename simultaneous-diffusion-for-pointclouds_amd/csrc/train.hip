@@ -652,29 +652,32 @@ int sdp_dsm_loss(const float* score, const float* noise, const float* mask, cons
 }
 
 int sdp_adam_ema_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, float* ema_shadow, size_t n,
-                      float lr, float beta1, float beta2, float eps, int step, float ema_mu, void* stream) {
+                      double lr, double beta1, double beta2, double eps, int step, double ema_mu, void* stream) {
   if (!params || !grads || !exp_avg || !exp_avg_sq || n == 0 || step < 1) return tfail("sdp_adam_ema_step: bad argument");
   return sdp_optim_ema_step(SDP_OPTIM_ADAM, params, grads, exp_avg, exp_avg_sq, nullptr, ema_shadow, n, lr, beta1, beta2,
-                            eps, 0.f, step, ema_mu, stream);
+                            eps, 0.0, step, ema_mu, stream);
 }
 
 int sdp_optim_ema_step(int kind, float* params, const float* grads, float* state0, float* state1, float* state2,
-                       float* ema_shadow, size_t n, float lr, float beta1, float beta2, float eps, float weight_decay,
-                       int step, float ema_mu, void* stream) {
+                       float* ema_shadow, size_t n, double lr, double beta1, double beta2, double eps,
+                       double weight_decay, int step, double ema_mu, void* stream) {
   if (!params || !grads || !state0 || n == 0 || step < 1 || kind < SDP_OPTIM_ADAM || kind > SDP_OPTIM_SGD ||
       (kind == SDP_OPTIM_ADAM && !state1))
     return tfail("sdp_optim_ema_step: bad argument");
   OptimHyper h{};
-  h.b1 = beta1;
-  h.b2 = beta2;
-  h.eps = eps;
-  h.weight_decay = weight_decay;
-  h.mu = ema_mu;
+  h.b1 = (float)beta1;
+  h.b2 = (float)beta2;
+  h.eps = (float)eps;
+  h.weight_decay = (float)weight_decay;
+  h.mu = (float)ema_mu;
+  h.omb1 = (float)(1.0 - beta1);
+  h.omb2 = (float)(1.0 - beta2);
+  h.ommu = (float)(1.0 - ema_mu);
   h.first = step == 1;
-  h.step_size = lr;
+  h.step_size = (float)lr;
   h.bc2_sqrt = 1.f;
   if (kind == SDP_OPTIM_ADAM) {   // torch: bias corrections in Python float (double), then lr / bc1, bc2 ** 0.5
-    const double bc1 = 1.0 - std::pow((double)beta1, step), bc2 = 1.0 - std::pow((double)beta2, step);
+    const double bc1 = 1.0 - std::pow(beta1, step), bc2 = 1.0 - std::pow(beta2, step);
     h.step_size = (float)(lr / bc1);
     h.bc2_sqrt = (float)std::sqrt(bc2);
   }

@@ -800,8 +800,8 @@ __global__ void optim_ema_kernel(float* __restrict__ p, const float* __restrict_
     if (h.weight_decay != 0.f) gi = gi + h.weight_decay * pi;   // torch._foreach_add(grads, params, alpha=wd)
     if constexpr (KIND == OPT_ADAM) {
       float mi = s0[i];
-      mi = mi + (1.f - h.b1) * (gi - mi);                        // lerp(m, g, 1-b1), weight < 0.5 branch
-      const float vi = s1[i] * h.b2 + (1.f - h.b2) * gi * gi;
+      mi = mi + h.omb1 * (gi - mi);                              // lerp(m, g, 1-b1), weight < 0.5 branch
+      const float vi = s1[i] * h.b2 + h.omb2 * gi * gi;
       s0[i] = mi;
       s1[i] = vi;
       float vd = vi;
@@ -812,16 +812,17 @@ __global__ void optim_ema_kernel(float* __restrict__ p, const float* __restrict_
       const float denom = sqrtf(vd) / h.bc2_sqrt + h.eps;
       pi = pi - h.step_size * (mi / denom);
     } else if constexpr (KIND == OPT_RMSPROP) {
-      const float vi = s0[i] * h.b2 + (1.f - h.b2) * gi * gi;   // b2 = alpha
+      const float vi = s0[i] * h.b2 + h.omb2 * gi * gi;         // b2 = alpha
       s0[i] = vi;
       pi = pi - h.step_size * (gi / (sqrtf(vi) + h.eps));
     } else {                                                      // SGD with momentum b1, dampening 0
-      const float bi = h.first ? gi : s0[i] * h.b1 + gi;
+      // torch: _foreach_mul_(bufs, momentum) then _foreach_add_(bufs, grads): two roundings, no FMA
+      const float bi = h.first ? gi : __fadd_rn(__fmul_rn(s0[i], h.b1), gi);
       s0[i] = bi;
       pi = pi - h.step_size * bi;
     }
     p[i] = pi;
-    if (shadow) shadow[i] = (1.f - h.mu) * pi + h.mu * shadow[i];
+    if (shadow) shadow[i] = h.ommu * pi + h.mu * shadow[i];
   }
 }
 

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("SDP_LIB", os.path.join(_HERE, "_lib", "libsdp.so"))
 P = C.c_void_p
 I = C.c_int
 F = C.c_float
+D = C.c_double
 U64 = C.c_uint64
 SZ = C.c_size_t
 
@@ -62,8 +63,8 @@ _SIGS = {
     "sdp_net_backward": (I, [P, P, I, P, SZ, P, P]),
     "sdp_net_backward_buckets": (I, [P, P, I, P, SZ, P, I, C.POINTER(SZ), C.POINTER(P), P]),
     "sdp_dsm_loss": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
-    "sdp_adam_ema_step": (I, [P, P, P, P, P, SZ, F, F, F, F, I, F, P]),
-    "sdp_optim_ema_step": (I, [I, P, P, P, P, P, P, SZ, F, F, F, F, F, I, F, P]),
+    "sdp_adam_ema_step": (I, [P, P, P, P, P, SZ, D, D, D, D, I, D, P]),
+    "sdp_optim_ema_step": (I, [I, P, P, P, P, P, P, SZ, D, D, D, D, D, I, D, P]),
     "sdp_range_project_workspace_size": (I, [I, I, C.POINTER(SZ)]),
     "sdp_range_project": (I, [P, I, I, I, P, I, I, P, P, P, P, P, P, SZ, P]),
     "sdp_view_transform": (I, [P, C.c_int64, P, P, P, P]),

@@ -385,3 +385,4 @@ def test_allforone_sampler_end_to_end_matches_golden(net256, setting, min_step):
     for got, k in zip(images + shared, ("new", "new2", "final", "shared0", "shared1")):
         want = f[k]
         assert _close_frac(got.numpy(), want, rtol=1e-4, atol=1e-4 * np.abs(want).max()) <= 1e-3, k
+

@@ -169,8 +169,11 @@ def test_get_optimizer_kinds_match_torch(name):
             if k == "step":
                 assert float(v) == float(ref_state["step"])
             else:
+                # same formula, rounding may differ by an ulp of the intermediates: absolute tolerance on the
+                # state's scale (a momentum sum that cancels to ~0 keeps the ulp of its terms)
                 n = v.numel()
-                assert torch.allclose(v.flatten(), ref_state[k].flatten()[off:off + n], rtol=1e-5, atol=1e-7), k
+                r = ref_state[k].flatten()
+                assert torch.allclose(v.flatten(), r[off:off + n], rtol=1e-5, atol=1e-6 * r.abs().max().item()), k
 
 
 def test_get_optimizer_unknown_raises():
