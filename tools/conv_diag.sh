@@ -8,10 +8,10 @@ for round in 1 2; do
   for ko in ${KOS:-0 1 2 4 16 31}; do
     for shape in "256 256 32 512" "128 128 64 1024"; do
       echo -n "round $round KO=$ko: "
-      timeout -k 5 60 tools/_cb/conv_bench_$ko $shape 4 1 40 ${MODE:-1} || exit 1
+      timeout -k 5 60 tools/_cb/conv_bench_$ko $shape ${BATCH:-4} 1 40 ${MODE:-1} || exit 1
     done
   done
 done
 for shape in "256 256 32 512" "128 128 64 1024"; do
-  timeout -k 5 60 tools/_cb/conv_bench_T $shape 4 1 40 ${MODE:-1} || exit 1
+  timeout -k 5 60 tools/_cb/conv_bench_T $shape ${BATCH:-4} 1 40 ${MODE:-1} || exit 1
 done
