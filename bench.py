@@ -18,7 +18,8 @@ Modes for line (one process per GPU; torchrun sets RANK/LOCAL_RANK/WORLD_SIZE):
       32 views on 8 GPUs = config 4); each rank owns 4 views, all-gathers the megabatch's
       images over RCCL every step (the cross-view consistency gather) and merges into its own.
   megabatch: every rank runs an independent megabatch (zero data exchange).
-Both: one 4-byte all_reduce(MAX) per step keeps the reference's global tooHigh exact.
+Both: one 4-byte all_reduce(MAX) per step keeps the reference's global tooHigh exact; it runs on a
+side stream beside the merge, whose final correction pass alone waits for it (sdp.merge.AbsmaxAllReduce).
 Per-GPU work is fixed as N grows ("scaling": "weak").  `value` = all views x steps / max-over-
 ranks wall time.  The dominant conv class is timed live with HIP events on the forward's
 stream (roofline); the CPU baseline is the oracle restatement timed on this host (rank 0, N=1).
@@ -146,28 +147,32 @@ def cpu_baseline_train(H, W, threads):
                       f"(torch CPU fp32), {dt:.2f} s"}
 
 
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
-
-
 def pmc_traffic(precision, V, cls):
     """HBM bytes per launch of the dominant conv class, read from the committed PMC passes
-    (tools/class_traffic.sh -> profiles/r03_traffic.json: TCC_EA0_RDREQ x 64 B x 2 (gfx950 wide-read
-    correction) + TCC_EA0_WRREQ bytes per launch of that kernel at this grid).  PMC counters cannot
-    be read inside this process, so the value is tagged with the hash of the conv kernel's sources
-    (sdp/_build.py conv_source_hash: common.h, conv_kernel.h, conv.hip -- what tools/conv_bench is
-    built from): when it does not match the current tree the traffic is reported as null (stale),
-    never as current."""
-    try:
-        with open(TRAFFIC_FILE) as f:
-            doc = json.load(f)
-    except OSError:
-        return None, None
+    (tools/class_traffic.sh -> profiles/rNN_traffic.json, newest round first: TCC_EA0_RDREQ x 64 B x 2
+    (gfx950 wide-read correction) + TCC_EA0_WRREQ bytes per launch of that kernel at this grid).  PMC
+    counters cannot be read inside this process, so the value is tagged with the hash of the conv
+    kernel's sources (sdp/_build.py conv_source_hash: common.h, conv_kernel.h, conv.hip -- what
+    tools/conv_bench is built from): when no file matches the current tree the traffic is reported as
+    null (stale), never as current."""
+    import glob
     from sdp import _build
-    if doc.get("conv_source_hash") != _build.conv_source_hash():
-        return None, f"stale: {os.path.basename(TRAFFIC_FILE)} was measured on another conv kernel source"
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_traffic.json")), reverse=True)
+    doc = None
+    for fn in files:
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if isinstance(d, dict) and d.get("conv_source_hash") == _build.conv_source_hash():
+            doc, src = d, fn
+            break
+    if doc is None:
+        return None, ("stale: no profiles/rNN_traffic.json was measured on this conv kernel source" if files else None)
     for r in doc.get("rows", []):
         if r.get("precision") == precision and r.get("views") == V and r.get("class") == cls:
-            return round(r["hbm_bytes"]), (f"{os.path.basename(TRAFFIC_FILE)} (PMC, conv source "
+            return round(r["hbm_bytes"]), (f"{os.path.basename(src)} (PMC, conv source "
                                            f"{doc['conv_source_hash'][:12]})")
     return None, None
 
@@ -196,7 +201,7 @@ def timed(step, args, dist, dev):
 
 def run_sampling(args, rank, N, dist, dev):
     from sdp import _lib
-    from sdp.merge import Merger, allforone_origins
+    from sdp.merge import AbsmaxAllReduce, Merger, allforone_origins
     from sdp.scorenet import ScoreNet
     from sdp.synthetic import exist_mask, scene_views
     from sdp.weights import get_sigmas_np
@@ -232,6 +237,7 @@ def run_sampling(args, rank, N, dist, dev):
     sig = get_sigmas_np()
     lik = torch.empty_like(x)
     absmax = torch.zeros(1, dtype=torch.int32, device=dev)
+    absmax_reduce = AbsmaxAllReduce()
     labels = {c: torch.full((V,), c, dtype=torch.int64, device=dev) for c in range(len(sig))}
     grad = torch.empty_like(x)
     L = _lib.lib()
@@ -254,18 +260,19 @@ def run_sampling(args, rank, N, dist, dev):
             net_box[0].forward_langevin(x, labels[c], ref, mask, None, seed, offset[0], float(s), float(ns), 1.0, True,
                                         lik, absmax)
         offset[0] += n_src * per_view4
+        ev = None
         if dist:
             if args.mode == "viewsplit":
                 torch.distributed.all_gather_into_tensor(x_all, x)     # cross-view consistency gather
-            torch.distributed.all_reduce(absmax, op=torch.distributed.ReduceOp.MAX)
+            ev = absmax_reduce(absmax)     # side stream; only the merge's correction pass waits for it
         if merge_ev is not None:
             ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ea.record()
-            merger(x_all, sig[c], setting, 10, 0.01, absmax)
+            merger(x_all, sig[c], setting, 10, 0.01, absmax, absmax_event=ev)
             eb.record()
             merge_ev.append((ea, eb))
         else:
-            merger(x_all, sig[c], setting, 10, 0.01, absmax)
+            merger(x_all, sig[c], setting, 10, 0.01, absmax, absmax_event=ev)
 
     # consistency merge (9 kernels on the forward's stream), SURVEY §8(d) compulsory bytes per
     # megabatch-step: per source view read x + mask + exist/sky, per output view write x and its

@@ -205,6 +205,16 @@ int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_ou
                           const uint8_t* exist, const uint8_t* sky, const int32_t* refmask,
                           const sdp_merge_params* params, const uint32_t* absmax_bits,
                           float* new_images, void* workspace, size_t workspace_bytes, void* stream);
+/* The same merge for multi-rank runs: the stream waits for absmax_event (a hipEvent_t
+ * recorded after the cross-rank all_reduce(MAX) of absmax_bits, or NULL) only right before the final
+ * correction pass, the merge's one reader of that word -- so the all_reduce on another stream runs
+ * beside the projection, binning and resolve passes instead of before them. */
+int sdp_consistency_merge_ev(float* x_all, int n_src, int aB, int o_begin, int n_out, int H, int W,
+                             const double* toWorld, const double* fromWorld, const float* origins,
+                             const uint8_t* exist, const uint8_t* sky, const int32_t* refmask,
+                             const sdp_merge_params* params, const uint32_t* absmax_bits,
+                             float* new_images, void* workspace, size_t workspace_bytes, void* stream,
+                             void* absmax_event);
 
 /* ---- point cloud -> range image (data front end; datasets/lidar_utils.py:54-347) --------
  * points: DEVICE float64 [N][stride] (x, y, z[, intensity]); origin: HOST float64 [3].

@@ -43,6 +43,9 @@ struct MergeArgs {
 };
 
 size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W);   // aB <= n_src
-hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why);
+// apply_wait (may be null): the stream waits for it right before the correction pass, the one reader
+// of a.absmax, so a cross-rank all_reduce(MAX) of that word can run beside the projection and binning
+hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why,
+                             hipEvent_t apply_wait = nullptr);
 
 }  // namespace sdp

@@ -456,7 +456,8 @@ size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   return b + 1024;
 }
 
-hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why) {
+hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_out, hipStream_t st, const char** why,
+                             hipEvent_t apply_wait) {
   const int H = a.g.H, W = a.g.W;
   const size_t cells = (size_t)a.g.big * W;
   if (ws_bytes < merge_ws_bytes(a.n_src, a.aB, a.n_out, H, W)) { *why = "merge: workspace too small"; return hipErrorInvalidValue; }
@@ -504,6 +505,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), 0, st, a, nb);
   hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), 0, st, a, nb);
   hipLaunchKernelGGL(merge_resolve_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
+  if (apply_wait && (e = hipStreamWaitEvent(st, apply_wait, 0)) != hipSuccess) return e;   // tooHigh's global max
   hipLaunchKernelGGL(merge_apply_kernel, dim3(grid_for(2 * nout)), dim3(256), 0, st, a);
   return hipGetLastError();
 }

@@ -53,10 +53,10 @@ int sdp_merge_workspace_bytes(int n_src, int aB, int n_out, int H, int W, size_t
   return 0;
 }
 
-int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_out, int H, int W, const double* toWorld,
-                          const double* fromWorld, const float* origins, const uint8_t* exist, const uint8_t* sky,
-                          const int32_t* refmask, const sdp_merge_params* prm, const uint32_t* absmax_bits,
-                          float* new_images, void* ws, size_t ws_bytes, void* stream) {
+int sdp_consistency_merge_ev(float* x_all, int n_src, int aB, int o_begin, int n_out, int H, int W, const double* toWorld,
+                             const double* fromWorld, const float* origins, const uint8_t* exist, const uint8_t* sky,
+                             const int32_t* refmask, const sdp_merge_params* prm, const uint32_t* absmax_bits,
+                             float* new_images, void* ws, size_t ws_bytes, void* stream, void* absmax_event) {
   if (!x_all || !prm || !exist || !sky || !refmask || !absmax_bits || !ws || aB <= 0 || n_out <= 0 || H <= 0 || W <= 0)
     return sdp_fail("sdp_consistency_merge: bad argument");
   if (prm->variant == SDP_MERGE_POSES && (!toWorld || !fromWorld))
@@ -101,9 +101,18 @@ int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_ou
   a.trig = trig;
   hipLaunchKernelGGL(merge_trig_kernel, dim3((W + H + 255) / 256), dim3(256), 0, st, trig, g, vMin);
   const char* why = "merge";
-  hipError_t e = consistency_merge(a, reinterpret_cast<char*>(ws) + tb, ws_bytes - tb, new_images, st, &why);
+  hipError_t e = consistency_merge(a, reinterpret_cast<char*>(ws) + tb, ws_bytes - tb, new_images, st, &why,
+                                   reinterpret_cast<hipEvent_t>(absmax_event));
   if (e != hipSuccess) return sdp_fail(std::string("sdp_consistency_merge: ") + why + " " + hipGetErrorString(e));
   return 0;
+}
+
+int sdp_consistency_merge(float* x_all, int n_src, int aB, int o_begin, int n_out, int H, int W, const double* toWorld,
+                          const double* fromWorld, const float* origins, const uint8_t* exist, const uint8_t* sky,
+                          const int32_t* refmask, const sdp_merge_params* prm, const uint32_t* absmax_bits,
+                          float* new_images, void* ws, size_t ws_bytes, void* stream) {
+  return sdp_consistency_merge_ev(x_all, n_src, aB, o_begin, n_out, H, W, toWorld, fromWorld, origins, exist, sky, refmask,
+                                  prm, absmax_bits, new_images, ws, ws_bytes, stream, nullptr);
 }
 
 }  // extern "C"

@@ -76,6 +76,7 @@ _SIGS = {
     "sdp_merge_workspace_size": (I, [I, I, I, I, C.POINTER(SZ)]),
     "sdp_merge_workspace_bytes": (I, [I, I, I, I, I, C.POINTER(SZ)]),
     "sdp_consistency_merge": (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, C.POINTER(MergeParams), P, P, P, SZ, P]),
+    "sdp_consistency_merge_ev": (I, [P, I, I, I, I, I, I, P, P, P, P, P, P, C.POINTER(MergeParams), P, P, P, SZ, P, P]),
 }
 
 _lib = None

@@ -52,11 +52,42 @@ class Merger:
         self.ws = torch.empty(n.value, dtype=torch.uint8, device=dev)
 
     def __call__(self, x: torch.Tensor, sigma, setting: int, allowance: float, cc: float, absmax: torch.Tensor,
-                 new_images: torch.Tensor | None = None) -> None:
-        """Correct x [B,2,H,W] in place (output views [o_begin, o_begin+n_out))."""
+                 new_images: torch.Tensor | None = None, absmax_event: torch.cuda.Event | None = None) -> None:
+        """Correct x [B,2,H,W] in place (output views [o_begin, o_begin+n_out)).  ``absmax_event``: the
+        final correction pass (the only reader of ``absmax``) waits for it (``AbsmaxAllReduce``)."""
         prm = _lib.MergeParams(self.variant, int(setting), float(np.float32(sigma)), float(allowance), float(cc))
-        _lib.check(_lib.lib().sdp_consistency_merge(
+        _lib.check(_lib.lib().sdp_consistency_merge_ev(
             x.data_ptr(), self.B, self.aB, self.o_begin, self.n_out, self.H, self.W,
             _lib.ptr(self.toWorld), _lib.ptr(self.fromWorld), _lib.ptr(self.origins),
             self.exist.data_ptr(), self.sky.data_ptr(), self.refmask.data_ptr(), _lib.C.byref(prm),
-            absmax.data_ptr(), _lib.ptr(new_images), self.ws.data_ptr(), self.ws.numel(), _lib.stream()), "merge")
+            absmax.data_ptr(), _lib.ptr(new_images), self.ws.data_ptr(), self.ws.numel(), _lib.stream(),
+            absmax_event.cuda_event if absmax_event is not None else None), "merge")
+
+
+class AbsmaxAllReduce:
+    """tooHigh's global max|x[:,0]| over the ranks (KITTISampling.py:162; one 4-byte all_reduce(MAX)
+    per merged step).  On GPUs the all_reduce runs on a side stream after the Langevin
+    update that wrote the word, and the returned event is handed to ``Merger`` so that only the merge's
+    final correction pass waits for it; the merge's projection and binning passes run meanwhile.  On
+    CPU tensors (gloo) it is the plain blocking all_reduce and returns None."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.comm = None
+        self.event = None
+
+    def __call__(self, absmax: torch.Tensor):
+        dist = torch.distributed
+        if not absmax.is_cuda:
+            dist.all_reduce(absmax, op=dist.ReduceOp.MAX, group=self.group)
+            return None
+        if self.comm is None:
+            self.comm = torch.cuda.Stream(device=absmax.device)
+            self.event = torch.cuda.Event()
+        self.comm.wait_stream(torch.cuda.current_stream(absmax.device))
+        with torch.cuda.stream(self.comm):
+            dist.all_reduce(absmax, op=dist.ReduceOp.MAX, group=self.group)
+            self.event.record()
+        # the next writer of absmax (the next step's zero_ on the current stream) is ordered after
+        # the merge's correction pass, which waits for this event
+        return self.event

@@ -27,7 +27,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .merge import Merger, allforone_origins
+from .merge import AbsmaxAllReduce, Merger, allforone_origins
 
 F32 = np.float32
 
@@ -189,6 +189,7 @@ def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr,
     images, shared = [], []
     L = len(sigmas)
     cc = cc0
+    absmax_reduce = AbsmaxAllReduce(dist_group)
     for c, sigma in enumerate(sigmas):
         cc = cc_ramp(cc, c, L)
         step = _step_size(step_lr, sigma, sigmas[-1])
@@ -199,11 +200,15 @@ def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr,
             if c >= min_step:
                 if view_split:
                     _gather_views(S, dist_group)
+                ev = None
                 if dist_group is not None or (view_split and torch.distributed.is_initialized()):
-                    torch.distributed.all_reduce(S.absmax, op=torch.distributed.ReduceOp.MAX, group=dist_group)
+                    ev = absmax_reduce(S.absmax)      # overlaps the merge up to its correction pass
                 want = c in (0, 20, 110) or c == L - 1
                 new = torch.empty(merger.n_out, S.C, S.H, S.W, device=S.dev) if want else None
-                merger(S.x_all, sigma, setting, allowance, cc, S.absmax, new)
+                if ev is None:
+                    merger(S.x_all, sigma, setting, allowance, cc, S.absmax, new)
+                else:
+                    merger(S.x_all, sigma, setting, allowance, cc, S.absmax, new, absmax_event=ev)
                 if c in (0, 20, 110):
                     shared.append(new.to("cpu"))
                 if c == L - 1:

@@ -386,3 +386,59 @@ def test_allforone_sampler_end_to_end_matches_golden(net256, setting, min_step):
         want = f[k]
         assert _close_frac(got.numpy(), want, rtol=1e-4, atol=1e-4 * np.abs(want).max()) <= 1e-3, k
 
+
+
+def _nccl_world1():
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    return dist
+
+
+def test_merge_absmax_event_orders_only_the_correction_pass():
+    """sdp_consistency_merge_ev (multi-rank tooHigh): the merge's correction pass waits
+    for the event of the all_reduce(MAX) running on another stream.  The side stream sleeps, then
+    raises absmax past tooHigh and all-reduces it (RCCL, world 1): the correction must see the raised
+    word (x unchanged); with AbsmaxAllReduce and no delay the result is bit-identical to the blocking
+    merge."""
+    from sdp.merge import AbsmaxAllReduce, Merger
+    dist = _nccl_world1()
+    try:
+        case = GI.merge_case("k_b4a4_s05", 4, 64, 256)
+        B, _, H, W = case["x"].shape
+        mk = lambda: Merger(B, 4, H, W, DEV, torch.from_numpy(case["exist"]), torch.from_numpy(case["sky"]),
+                            torch.from_numpy(case["mask"]), toWorld=torch.from_numpy(case["toWorld"]),
+                            fromWorld=torch.from_numpy(case["fromWorld"]))
+        low = np.abs(_after_update(case)[:, 0]).max()
+        bits = lambda v: torch.tensor([v], dtype=torch.float32).view(torch.int32).to(DEV)
+        # 1. ordering: the raised word arrives late on the side stream
+        m = mk()
+        x = torch.from_numpy(_after_update(case)).to(DEV)
+        absmax = bits(low)
+        comm, ev = torch.cuda.Stream(), torch.cuda.Event()
+        comm.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(comm):
+            torch.cuda._sleep(100_000_000)
+            absmax.copy_(bits(9.0))                       # 9*6/1 > 50: tooHigh
+            dist.all_reduce(absmax, op=dist.ReduceOp.MAX)
+            ev.record()
+        m(x, 0.5, 5, 10, 0.01, absmax, None, absmax_event=ev)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(x.cpu().numpy(), _after_update(case))
+        # 2. AbsmaxAllReduce + the event form == the blocking merge, bit for bit
+        new_ref, x_ref = _gpu_merge(case, 4, 0.5, 5, 10, 0.01)
+        m = mk()
+        x = torch.from_numpy(_after_update(case)).to(DEV)
+        absmax = bits(low)
+        new = torch.empty(B, 2, H, W, device=DEV)
+        ev = AbsmaxAllReduce()(absmax)
+        m(x, 0.5, 5, 10, 0.01, absmax, new, absmax_event=ev)
+        np.testing.assert_array_equal(x.cpu().numpy(), x_ref)
+        np.testing.assert_array_equal(new.cpu().numpy(), new_ref)
+        assert not np.array_equal(x_ref, _after_update(case))   # (the correction did run)
+    finally:
+        dist.destroy_process_group()

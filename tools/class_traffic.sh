@@ -7,7 +7,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 O=gpurun_out/class_traffic
 mkdir -p $O
 for mode in 1 0; do
