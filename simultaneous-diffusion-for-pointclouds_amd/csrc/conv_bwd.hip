@@ -14,6 +14,7 @@
 #define SDP_DGRAD_TC_WM1 64
 #endif
 
+
 namespace sdp {
 
 // 8 x 16 pixel tiles (the forward's: a 10 x 18 patch, 1.41x the pixels, against 4 x 66 = 2.06x for
@@ -26,6 +27,10 @@ namespace sdp {
 
 template <int MODE>
 static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, bool t16, hipStream_t st) {
+#ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: the 8 x 16 circular 3x3 data gradients only
+  if (!t16) return hipErrorInvalidValue;
+  return wm == 2 ? dgrad_launch_half<MODE>(a, st) : dgrad_launch<MODE, 1, 16, 3, false>(a, st);
+#endif
   if (ks == 1) return dgrad_launch<MODE, 2, 32, 1, false>(a, st);
   if (!a.circular) return dgrad_launch<MODE, 2, 32, 3, true>(a, st);
   if (t16) return wm == 2 ? dgrad_launch_half<MODE>(a, st) : dgrad_launch<MODE, 1, 16, 3, false>(a, st);

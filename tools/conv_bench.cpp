@@ -1,6 +1,7 @@
 // Standalone timing of one conv_mfma launch shape (diagnostics; links a conv.o built with
 // -DSDP_CONV_BENCH_ONLY [-DSDP_KO=mask]).  Usage: conv_bench Cin Cout H W B [dil] [iters] [mode]
-// (mode: 0 fp32, 1 fp32x3 (default), 2 bf16)
+// (mode: 0 fp32, 1 fp32x3 (default), 2 bf16) [dgrad]: with a 9th argument "dgrad", the data gradient
+// (conv_dgrad: no prologue, epilogue * elu'(IN++ input, dact 3) + residual, as the training backward)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -59,16 +60,32 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 3; ++i) CK(sdp::conv_mfma(mode, a, 3, false, 0, &why));
+  const bool dg = argc > 9 && !strcmp(argv[9], "dgrad");
+  if (dg) {   // the training data gradient: dy in, dx = conv^T(dy) * elu'(h * scale + shift) + res
+    float *aux, *res, *ess;
+    CK(hipMalloc(&aux, nout * 4));
+    CK(hipMalloc(&res, nout * 4));
+    CK(hipMalloc(&ess, (size_t)B * Cout * 2 * 4));
+    CK(hipMemcpy(aux, h.data(), std::min(nin, nout) * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(res, 0, nout * 4));
+    std::vector<float> e2((size_t)B * Cout * 2);
+    for (size_t i = 0; i < e2.size(); i += 2) { e2[i] = 1.f; e2[i + 1] = 0.f; }
+    CK(hipMemcpy(ess, e2.data(), e2.size() * 4, hipMemcpyHostToDevice));
+    a.wf16 = nullptr; a.pro_mode = sdp::PRO_NONE; a.stats = nullptr; a.bias = nullptr;
+    a.dact = 3; a.aux = aux; a.epi_ss = ess; a.res = res;
+  }
+  auto launch = [&]() { return dg ? sdp::conv_dgrad(mode, a, 3, 0, &why) : sdp::conv_mfma(mode, a, 3, false, 0, &why); };
+  for (int i = 0; i < 3; ++i) CK(launch());
   CK(hipDeviceSynchronize());
   CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(sdp::conv_mfma(mode, a, 3, false, 0, &why));
+  for (int i = 0; i < iters; ++i) CK(launch());
   CK(hipEventRecord(e1, 0));
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = ms * 1e3 / iters, fl = 2.0 * B * H * W * (double)Cin * Cout * 9;
-  printf("conv %d->%d @%dx%d B=%d d=%d mode %d: %.1f us  %.1f TF/s (algorithmic)\n", Cin, Cout, H, W, B, dil, mode, us,
+  printf("%s %d->%d @%dx%d B=%d d=%d mode %d: %.1f us  %.1f TF/s (algorithmic)\n", dg ? "dgrad" : "conv", Cin, Cout, H,
+         W, B, dil, mode, us,
          fl / us * 1e-6);
 #ifdef SDP_TIMING
   std::vector<unsigned long long> d((size_t)nwg_max * 8);
