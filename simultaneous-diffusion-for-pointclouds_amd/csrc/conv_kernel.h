@@ -691,21 +691,37 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     constexpr int PER = POOL ? 2 : 4;                // values per fragment and lane
     constexpr int NV = NF * PER;
     const int xs = (POOL ? 1 : d) * Cout * 4;        // bytes between consecutive output pixels of a run
+    // byte offset of value i of channel block nj: a per-fragment VGPR base (channel block 0) and a
+    // wave-uniform SGPR part (the value's pixel step, the block's 64-B channel offset)
+    int vbase[NF];
+    static_for<0, NF>([&](auto fc) {
+      constexpr int f = decltype(fc)::value;
+      const int co = n0 + wn * 64 + lcol;
+      if constexpr (POOL) {
+        vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 16) >> 1) + 2 * lq) * Cout + co) * 4;
+      } else {
+        constexpr int mr = f / CB, mc = (f % CB) * 16;
+        const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lq) * d + ph_c;
+        vbase[f] = ((y * Wo + x) * Cout + co) * 4;
+      }
+    });
+#define SDP_EPI16_OFF(i, nj) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs + (nj) * 64)
+    // The addend of every channel block (the residual, else the CRP second output's res2) is loaded
+    // before the first store: loads and stores retire through one in-order counter on gfx9, so a
+    // block's loads issued after the previous block's stores would wait for their acknowledgement too
+    float pre[4][NV];
+    if (a.res || a.out2) {
+      const __amdgpu_buffer_rsrc_t prs = a.res ? rrs : r2rs;
+      static_for<0, 4>([&](auto njc) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          pre[njc][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, SDP_EPI16_OFF(i, decltype(njc)::value), 0));
+      });
+    }
     static_for<0, 4>([&](auto njc) {
       constexpr int nj = decltype(njc)::value;
       const int co = n0 + wn * 64 + nj * 16 + lcol;
       const float bias = a.bias ? a.bias[co] : 0.f;
-      int vbase[NF];
-      static_for<0, NF>([&](auto fc) {
-        constexpr int f = decltype(fc)::value;
-        if constexpr (POOL) {
-          vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 16) >> 1) + 2 * lq) * Cout + co) * 4;
-        } else {
-          constexpr int mr = f / CB, mc = (f % CB) * 16;
-          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lq) * d + ph_c;
-          vbase[f] = ((y * Wo + x) * Cout + co) * 4;
-        }
-      });
       float v[NV];
       if constexpr (POOL) {
         static_for<0, CB>([&](auto fc) {
@@ -743,7 +759,6 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           v[i] = v[i] + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
         }
       }
-#define SDP_EPI16_OFF(i) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs)
       if (a.dact) {   // backward: * the derivative of the ELU that followed this tensor (ConvArgs::dact)
         float esc = 1.f, esh = 0.f;
         if (a.dact == 3) {
@@ -752,21 +767,22 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-          float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI16_OFF(i), 0));
+          float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI16_OFF(i, nj), 0));
           if (a.dact == 3) h = fmaf(h, esc, esh);
           v[i] = v[i] * elu_grad(h, a.dact);
         }
       }
       if (a.res) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, SDP_EPI16_OFF(i), 0)) + v[i];
+        for (int i = 0; i < NV; ++i) v[i] = pre[nj][i] + v[i];
       }
       if (a.out2) {
+        float r2[NV];
 #pragma unroll
-        for (int i = 0; i < NV; ++i) {
-          const float r2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI16_OFF(i), 0));
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2), o2rs, SDP_EPI16_OFF(i), 0);
-        }
+        for (int i = 0; i < NV; ++i)   // (a residual and a second output together: loaded here, all before the stores)
+          r2[i] = a.res ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI16_OFF(i, nj), 0)) : pre[nj][i];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2[i]), o2rs, SDP_EPI16_OFF(i, nj), 0);
       }
       if (a.epi_elu) {
 #pragma unroll
@@ -774,9 +790,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
       }
       if constexpr (!(SDP_KO & 16)) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI16_OFF(i), SDP_STORE_AUX);
+        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI16_OFF(i, nj), SDP_STORE_AUX);
       }
-#undef SDP_EPI16_OFF
       if (a.stats) {
         float sum = 0.f;
 #pragma unroll
@@ -803,6 +818,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         }
       }
     });
+#undef SDP_EPI16_OFF
     }  // if constexpr (SH == 16 && !TRANS)
   } else if (a.dact) {
     if constexpr (TC >= 32 && NW == 4 && SH == 16) {   // (the data gradient runs in the bf16 modes only)
@@ -1016,24 +1032,37 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
       constexpr int PER = POOL ? 8 : 16;
       // byte offset step between consecutive output pixels of a fragment row (wave-uniform)
       const int xs = (POOL ? 1 : d) * Cout * 4;
+      int vbase[POOL ? CB : 4];                          // byte offset of the fragment's pixel m = 4*lhalf (block nb = 0)
+      static_for<0, (POOL ? CB : 4)>([&](auto fc) {
+        constexpr int f = decltype(fc)::value;
+        const int co = n0 + wn * 64 + lcol;
+        if constexpr (POOL) {
+          vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 32) >> 1) + 2 * lhalf) * Cout + co) * 4;
+        } else {
+          constexpr int mr = f / CB, mc = (f % CB) * 32;
+          const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lhalf) * d + ph_c;
+          vbase[f] = ((y * Wo + x) * Cout + co) * 4;
+        }
+      });
+      // pixel index (within the fragment row, relative to 4*lhalf) of value step k
+      auto mstep = [](int k) { return POOL ? ((((k & 1) * 2 + (k >> 1) * 4) & 3) + 8 * (((k & 1) * 2 + (k >> 1) * 4) >> 2)) / 2
+                                           : (k & 3) + 8 * (k >> 2); };
+  #define SDP_EPI_OFF(i, nb) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(mstep((i) % PER) * xs + (nb) * 128)
+      // the addend of both channel blocks (residual, else res2) loaded before the first store (see
+      // the 16x16 epilogue: loads and stores retire in one in-order counter)
+      float pre[2][NV];
+      if (a.res || a.out2) {
+        const __amdgpu_buffer_rsrc_t prs = a.res ? rrs : r2rs;
+        static_for<0, 2>([&](auto nbc) {
+  #pragma unroll
+          for (int i = 0; i < NV; ++i)
+            pre[nbc][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, SDP_EPI_OFF(i, decltype(nbc)::value), 0));
+        });
+      }
       static_for<0, 2>([&](auto nbc) {
         constexpr int nb = decltype(nbc)::value;
         const int co = n0 + wn * 64 + nb * 32 + lcol;
         const float bias = a.bias ? a.bias[co] : 0.f;
-        int vbase[POOL ? CB : 4];                        // byte offset of the fragment's pixel m = 4*lhalf
-        static_for<0, (POOL ? CB : 4)>([&](auto fc) {
-          constexpr int f = decltype(fc)::value;
-          if constexpr (POOL) {
-            vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 32) >> 1) + 2 * lhalf) * Cout + co) * 4;
-          } else {
-            constexpr int mr = f / CB, mc = (f % CB) * 32;
-            const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lhalf) * d + ph_c;
-            vbase[f] = ((y * Wo + x) * Cout + co) * 4;
-          }
-        });
-        // pixel index (within the fragment row, relative to 4*lhalf) of value step k
-        auto mstep = [](int k) { return POOL ? ((((k & 1) * 2 + (k >> 1) * 4) & 3) + 8 * (((k & 1) * 2 + (k >> 1) * 4) >> 2)) / 2
-                                             : (k & 3) + 8 * (k >> 2); };
         float v[NV];
         if constexpr (POOL) {
           static_for<0, CB>([&](auto mbc) {
@@ -1072,7 +1101,6 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
             v[i] = v[i] + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
           }
         }
-  #define SDP_EPI_OFF(i) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(mstep((i) % PER) * xs)
         if (a.dact) {
           float esc = 1.f, esh = 0.f;
           if (a.dact == 3) {
@@ -1081,21 +1109,22 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           }
   #pragma unroll
           for (int i = 0; i < NV; ++i) {
-            float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI_OFF(i), 0));
+            float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI_OFF(i, nb), 0));
             if (a.dact == 3) h = fmaf(h, esc, esh);
             v[i] = v[i] * elu_grad(h, a.dact);
           }
         }
         if (a.res) {
   #pragma unroll
-          for (int i = 0; i < NV; ++i) v[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, SDP_EPI_OFF(i), 0)) + v[i];
+          for (int i = 0; i < NV; ++i) v[i] = pre[nb][i] + v[i];
         }
         if (a.out2) {
+          float r2[NV];
   #pragma unroll
-          for (int i = 0; i < NV; ++i) {
-            const float r2 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI_OFF(i), 0));
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2), o2rs, SDP_EPI_OFF(i), 0);
-          }
+          for (int i = 0; i < NV; ++i)
+            r2[i] = a.res ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI_OFF(i, nb), 0)) : pre[nb][i];
+  #pragma unroll
+          for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2[i]), o2rs, SDP_EPI_OFF(i, nb), 0);
         }
         if (a.epi_elu) {
   #pragma unroll
@@ -1103,9 +1132,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         }
         if constexpr (!(SDP_KO & 16)) {
   #pragma unroll
-          for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI_OFF(i), SDP_STORE_AUX);
+          for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI_OFF(i, nb), SDP_STORE_AUX);
         }
-  #undef SDP_EPI_OFF
         if (a.stats) {
           float sum = 0.f;
   #pragma unroll
@@ -1127,6 +1155,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           }
         }
       });
+  #undef SDP_EPI_OFF
     }
     }  // if constexpr (SH == 32)
   }

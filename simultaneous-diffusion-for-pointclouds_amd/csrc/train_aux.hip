@@ -247,8 +247,11 @@ __global__ void inpp_bwd_params_kernel(const float* __restrict__ ppart, int B, i
 // out = k1*g + k2*(h - mean) + k3 (+ r1) (+ r2).  Grid (blocks, B): a thread's channel group is
 // fixed (the block stride is a multiple of C/4), so its 4 coefficient rows are loaded once per image
 __global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ h,
-                                                             const float4* __restrict__ coef, const float* r1,
-                                                             const float* r2, float* out, int HW, int C) {
+                                                             const float4* __restrict__ coef, const float* __restrict__ r1,
+                                                             const float* __restrict__ r2, float* __restrict__ out, int HW,
+                                                             int C) {
+  // (__restrict__ on every operand -- the calls are elementwise, so even an in-place one is safe --
+  // lets the next iteration's loads issue before this one's store: loads and stores retire in order)
   const int C4 = C / 4;
   const int b = blockIdx.y;
   const size_t n4 = (size_t)HW * C4, off = (size_t)b * n4;
@@ -458,8 +461,9 @@ __global__ void upsample_bwd_kernel(const float* __restrict__ g, float* __restri
 }
 
 // dst = dy * elu'(from the ELU output y) (+ res)
-__global__ void elu_bwd_post_kernel(const float* __restrict__ dy, const float* __restrict__ y, const float* res,
-                                    float* dst, size_t n4) {
+__global__ void elu_bwd_post_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                    const float* __restrict__ res, float* __restrict__ dst, size_t n4) {
+#pragma unroll 2
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const float4 d = reinterpret_cast<const float4*>(dy)[i], yv = reinterpret_cast<const float4*>(y)[i];
     float4 v = make_float4(d.x * elu_grad(yv.x, 2), d.y * elu_grad(yv.y, 2), d.z * elu_grad(yv.z, 2),
@@ -473,7 +477,8 @@ __global__ void elu_bwd_post_kernel(const float* __restrict__ dy, const float* _
 }
 
 // dst = a + b (float4 lanes)
-__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* dst, size_t n4) {
+__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ dst, size_t n4) {
+#pragma unroll 2
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const float4 x = reinterpret_cast<const float4*>(a)[i], y = reinterpret_cast<const float4*>(b)[i];
     reinterpret_cast<float4*>(dst)[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
