@@ -706,10 +706,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
       }
     });
 #define SDP_EPI16_OFF(i, nj) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs + (nj) * 64)
-    // The addend of every channel block (the residual, else the CRP second output's res2) is loaded
-    // before the first store: loads and stores retire through one in-order counter on gfx9, so a
-    // block's loads issued after the previous block's stores would wait for their acknowledgement too
-    float pre[4][NV];
+    // The bias and the addend of every channel block (the residual, else the CRP second output's res2)
+    // are loaded before the first store: loads and stores retire through one in-order counter on gfx9,
+    // so a block's loads issued after the previous block's stores would wait for their acknowledgement
+    // too (line 328.2 -> 335.1 image-steps/s, profiles/experiments/r04_epilogue_preload_ab.log)
+    float pre[4][NV], biasv[4];
+    static_for<0, 4>([&](auto nj) { biasv[nj] = a.bias ? a.bias[n0 + wn * 64 + nj * 16 + lcol] : 0.f; });
     if (a.res || a.out2) {
       const __amdgpu_buffer_rsrc_t prs = a.res ? rrs : r2rs;
       static_for<0, 4>([&](auto njc) {
@@ -721,7 +723,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     static_for<0, 4>([&](auto njc) {
       constexpr int nj = decltype(njc)::value;
       const int co = n0 + wn * 64 + nj * 16 + lcol;
-      const float bias = a.bias ? a.bias[co] : 0.f;
+      const float bias = biasv[nj];
       float v[NV];
       if constexpr (POOL) {
         static_for<0, CB>([&](auto fc) {
@@ -1050,7 +1052,8 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   #define SDP_EPI_OFF(i, nb) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(mstep((i) % PER) * xs + (nb) * 128)
       // the addend of both channel blocks (residual, else res2) loaded before the first store (see
       // the 16x16 epilogue: loads and stores retire in one in-order counter)
-      float pre[2][NV];
+      float pre[2][NV], biasv[2];
+      static_for<0, 2>([&](auto nb) { biasv[nb] = a.bias ? a.bias[n0 + wn * 64 + nb * 32 + lcol] : 0.f; });
       if (a.res || a.out2) {
         const __amdgpu_buffer_rsrc_t prs = a.res ? rrs : r2rs;
         static_for<0, 2>([&](auto nbc) {
@@ -1062,7 +1065,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
       static_for<0, 2>([&](auto nbc) {
         constexpr int nb = decltype(nbc)::value;
         const int co = n0 + wn * 64 + nb * 32 + lcol;
-        const float bias = a.bias ? a.bias[co] : 0.f;
+        const float bias = biasv[nb];
         float v[NV];
         if constexpr (POOL) {
           static_for<0, CB>([&](auto mbc) {
