@@ -845,6 +845,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     const int cg = tid % CG, pl = tid / CG;
     const int co0 = n0 + cg * 4;                     // this thread's 4 output channels
     const float4 bias4 = a.bias ? ld4(a.bias + co0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 es0 = make_float4(1.f, 0.f, 1.f, 0.f), es1 = es0;   // (scale, shift) of the thread's 4 channels (dact 3)
+    if (a.dact == 3) {
+      es0 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2);
+      es1 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2 + 4);
+    }
     const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
     float* outb = a.out + (size_t)b * Ho * Wo * Cout;
     // shifted sums per (stats group, channel): K = the thread's first value
@@ -884,12 +889,43 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
       }
       __syncthreads();
       // ---- row phase: output pixels j = pl, pl + PL, ... of this half
-  #pragma unroll 2
+      auto pix = [&](int j, int& y, int& x, int& g) __attribute__((always_inline)) {
+        if constexpr (POOL) {   // staged pixel s = row*32 + col over rows 0/1 and columns [32h, 32h+32)
+          y = (sr0 + wrow0) >> 1;
+          x = (sc0 + 32 * h + 2 * j) >> 1;
+          g = 0;
+        } else {
+          const int ws = j >> 6, q = j & 63;                 // staged pixel -> (wave row block, pixel)
+          const int mb = 2 * h + (q >> 5);
+          const int row = ws * T::RW + mb / (TC / 32), col = (mb % (TC / 32)) * 32 + (q & 31);
+          y = (sr0 + row) * d + ph_r;
+          x = (sc0 + col) * d + ph_c;
+          g = ws;
+        }
+      };
+      const size_t bo = (size_t)b * Ho * Wo * Cout;
+      // the elu' operand, the residual and res2 of the NEXT pixel are loaded before this pixel's
+      // stores: loads and stores retire in order (vmcnt), so loads issued after the stores would wait
+      // for their acknowledgement -- a store + load round trip per pixel
+      struct Ops { float4 h, r, q; };
+      auto fetch = [&](int j) __attribute__((always_inline)) {
+        Ops o;
+        int y, x, g;
+        pix(min(j, NPO - 1), y, x, g);
+        const size_t oi = bo + ((size_t)y * Wo + x) * Cout + co0;
+        o.h = a.aux ? ld4(a.aux + oi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        o.r = a.res ? ld4(a.res + oi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        o.q = a.out2 ? ld4(a.res2 + oi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        return o;
+      };
+      Ops nx = fetch(pl);
       for (int j = pl; j < NPO; j += PL) {
+        const Ops cu = nx;
+        nx = fetch(j + PL);
         float4 v;
         int y, x, g;
+        pix(j, y, x, g);
         if constexpr (POOL) {
-          // staged pixel s = row*32 + col over rows 0/1 and columns [32h, 32h+32)
           const float* s0 = stage + (2 * j) * SROW + cg * 4;
           const float4 o00 = ld4(s0), o01 = ld4(s0 + SROW), o10 = ld4(s0 + 32 * SROW), o11 = ld4(s0 + 33 * SROW);
           auto pool1 = [&](float a00, float a10, float a01, float a11, float bb) {
@@ -899,18 +935,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           v.y = pool1(o00.y, o10.y, o01.y, o11.y, bias4.y);
           v.z = pool1(o00.z, o10.z, o01.z, o11.z, bias4.z);
           v.w = pool1(o00.w, o10.w, o01.w, o11.w, bias4.w);
-          y = (sr0 + wrow0) >> 1;
-          x = (sc0 + 32 * h + 2 * j) >> 1;
-          g = 0;
         } else {
           const float4 o = ld4(stage + j * SROW + cg * 4);
           v = make_float4(o.x + bias4.x, o.y + bias4.y, o.z + bias4.z, o.w + bias4.w);
-          const int ws = j >> 6, q = j & 63;                 // staged pixel -> (wave row block, pixel)
-          const int mb = 2 * h + (q >> 5);
-          const int row = ws * T::RW + mb / (TC / 32), col = (mb % (TC / 32)) * 32 + (q & 31);
-          y = (sr0 + row) * d + ph_r;
-          x = (sc0 + col) * d + ph_c;
-          g = ws;
         }
         const size_t oidx = ((size_t)y * Wo + x) * Cout + co0;
         if (a.up) {
@@ -933,28 +960,21 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           v.z = v.z + bil(v00.z, v01.z, v10.z, v11.z);
           v.w = v.w + bil(v00.w, v01.w, v10.w, v11.w);
         }
-        const size_t bo = (size_t)b * Ho * Wo * Cout;
         if (a.dact) {
           // backward: scale by the derivative of the ELU that followed this tensor in the forward
           //   1: aux = pre-activation h          elu'(h) = h > 0 ? 1 : e^h
           //   2: aux = post-activation ELU(h)    elu'    = y > 0 ? 1 : y + 1
           //   3: aux = InstanceNorm++ input h, z = h*scale + shift (epi_ss)  elu'(z)
-          float4 h4 = ld4(a.aux + bo + oidx);
-          if (a.dact == 3) {
-            const float4 s0 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2), s1 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2 + 4);
-            h4 = make_float4(fmaf(h4.x, s0.x, s0.y), fmaf(h4.y, s0.z, s0.w), fmaf(h4.z, s1.x, s1.y), fmaf(h4.w, s1.z, s1.w));
-          }
+          float4 h4 = cu.h;
+          if (a.dact == 3)
+            h4 = make_float4(fmaf(h4.x, es0.x, es0.y), fmaf(h4.y, es0.z, es0.w), fmaf(h4.z, es1.x, es1.y),
+                             fmaf(h4.w, es1.z, es1.w));
           v = make_float4(v.x * elu_grad(h4.x, a.dact), v.y * elu_grad(h4.y, a.dact), v.z * elu_grad(h4.z, a.dact),
                           v.w * elu_grad(h4.w, a.dact));
         }
-        if (a.res) {
-          const float4 r4 = ld4(a.res + bo + oidx);
-          v = make_float4(r4.x + v.x, r4.y + v.y, r4.z + v.z, r4.w + v.w);
-        }
-        if (a.out2) {
-          const float4 r4 = ld4(a.res2 + bo + oidx);
-          *reinterpret_cast<float4*>(a.out2 + bo + oidx) = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
-        }
+        if (a.res) v = make_float4(cu.r.x + v.x, cu.r.y + v.y, cu.r.z + v.z, cu.r.w + v.w);
+        if (a.out2)
+          *reinterpret_cast<float4*>(a.out2 + bo + oidx) = make_float4(v.x + cu.q.x, v.y + cu.q.y, v.z + cu.q.z, v.w + cu.q.w);
         if (a.epi_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
         if constexpr (!(SDP_KO & 16)) *reinterpret_cast<float4*>(outb + oidx) = v;
         static_for<0, WM>([&](auto gc) {

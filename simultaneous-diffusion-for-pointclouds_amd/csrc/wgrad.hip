@@ -193,6 +193,12 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     const float4* ra = raS[SET];
     const int sb = tb, sr0_ = tsr0, sc0_ = tsc0;
     const float* ssb = a.pro_ss + (size_t)sb * a.ss_bstride + ci0 * 2;
+    // every unit of a thread has channel group cv = tid % 8: its (scale, shift) loaded once
+    float4 s0 = make_float4(1.f, 0.f, 1.f, 0.f), s1 = s0;
+    if (a.pro_mode != PRO_NONE) {
+      s0 = *reinterpret_cast<const float4*>(ssb + (tid & 7) * 8);
+      s1 = *reinterpret_cast<const float4*>(ssb + (tid & 7) * 8 + 4);
+    }
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
       const int u = tid + k * 256;
@@ -200,8 +206,6 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       const int pix = u >> 3, cv = u & 7;
       float4 v = ra[k];
       if (a.pro_mode != PRO_NONE) {
-        const float4 s0 = *reinterpret_cast<const float4*>(ssb + cv * 8);
-        const float4 s1 = *reinterpret_cast<const float4*>(ssb + cv * 8 + 4);
         v = make_float4(fmaf(v.x, s0.x, s0.y), fmaf(v.y, s0.z, s0.w), fmaf(v.z, s1.x, s1.y), fmaf(v.w, s1.z, s1.w));
         v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
       }
@@ -217,8 +221,11 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
   using INA = std::integral_constant<int, T::NUA>;
   // OCC 2: two workgroups per CU take turns (one stages while the other's MFMAs run), so a
   // tile is staged in chunks of CH units straight through registers, no cross-tile prefetch
+  // (8 units = 32 VGPRs of loads: with the 144 accumulators at two waves per SIMD, 11 units spill
+  // 3 VGPRs, a whole tile (22 units) 75)
   constexpr int CH = 8;
   auto stage_chunked = [&]() {
+
     static_for<0, (T::NUD + CH - 1) / CH>([&](auto c) {
       using KB = std::integral_constant<int, decltype(c)::value * CH>;
       using KE = std::integral_constant<int, (decltype(c)::value * CH + CH < T::NUD ? decltype(c)::value * CH + CH : T::NUD)>;
