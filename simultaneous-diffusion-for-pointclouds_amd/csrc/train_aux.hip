@@ -101,7 +101,9 @@ __global__ void pack_weights_multi_kernel(const PackDesc* __restrict__ d, int mo
 hipError_t pack_weights_multi(const PackDesc* d, int nd, size_t total, int mode, hipStream_t st) {
   if (nd <= 0) return hipSuccess;
   (void)total;
-  hipLaunchKernelGGL(pack_weights_multi_kernel, dim3(64, nd), dim3(256), 0, st, d, mode);
+  // 512 blocks per conv: each thread re-packs a few slots (its loads wait behind its previous
+  // slot's store -- loads and stores retire in order -- so the chain per thread is kept short)
+  hipLaunchKernelGGL(pack_weights_multi_kernel, dim3(512, nd), dim3(256), 0, st, d, mode);
   return hipGetLastError();
 }
 
