@@ -201,7 +201,8 @@ def gen_allforone():
         return torch.zeros_like(x)
 
     B = aB = 7
-    for tag, sigma, setting in [("a_b7_s05_set7", 0.5, 7), ("a_b7_s05_set5", 0.5, 5)]:
+    # setting 8: the controlled average with allowance 5 (models/__init__.py:469-470)
+    for tag, sigma, setting in [("a_b7_s05_set7", 0.5, 7), ("a_b7_s05_set5", 0.5, 5), ("a_b7_s05_set8", 0.5, 8)]:
         case = GI.merge_case(tag, B, 64, 256)
         with torch.no_grad(), _NoiseFeed("merge"):
             imgs, _, _ = models.anneal_Langevin_dynamics_inpainting_simultaneous_basic(
@@ -261,24 +262,30 @@ def gen_config1():
          final=imgs[6].numpy())
 
 
+# kitti sampler end to end: (tag, setting, file).  Setting 5 keeps cc; setting 7 ramps
+# cc = 0.5 / (L / (c + 1)) over the levels (KITTISampling.py:106-109)
+KITTI_E2E = [("e2e", 5, "kitti_e2e_b2_64x256.npz"), ("e2e_set7", 7, "kitti_e2e_set7_b2_64x256.npz")]
+
+
 def gen_kitti_e2e():
     """Simultaneous kitti sampler end to end: B=aB=2, 3 levels x 2 steps + denoise (64x256)."""
     from models.KITTISampling import anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti as S
     H, W, B = 64, 256, 2
     m = build_net(128, H, W)
-    case = GI.merge_case("e2e", B, H, W)
-    x0 = GI.scorenet_input("e2e", B, H, W)
     sig = get_sigmas_np()[229:232]
-    with torch.no_grad(), _NoiseFeed("e2e"):
-        imgs, _, shared = S(torch.from_numpy(x0), torch.from_numpy(case["ref"]), torch.from_numpy(case["mask"]),
-                            torch.from_numpy(case["sky"]), None, 2, 5, 10, m, sig,
-                            torch.from_numpy(case["fromWorld"].reshape(B, 1, 4, 4)),
-                            torch.from_numpy(case["toWorld"].reshape(B, 1, 4, 4)), B,
-                            n_steps_each=2, step_lr=6.2e-6, existMask=torch.from_numpy(case["exist"]),
-                            denoise=True, verbose=False, grad_ref=1, correlation_coefficient=0.01)
-    # images = [newImages (last level, step 1), newImages (step 2), final x]  (KITTISampling.py:418-419, 511)
-    assert len(imgs) == 3
-    save("kitti_e2e_b2_64x256.npz", new=imgs[0].numpy(), new2=imgs[1].numpy(), final=imgs[2].numpy())
+    for tag, setting, fname in KITTI_E2E:
+        case = GI.merge_case(tag, B, H, W)
+        x0 = GI.scorenet_input(tag, B, H, W)
+        with torch.no_grad(), _NoiseFeed(tag):
+            imgs, _, shared = S(torch.from_numpy(x0), torch.from_numpy(case["ref"]), torch.from_numpy(case["mask"]),
+                                torch.from_numpy(case["sky"]), None, 2, setting, 10, m, sig,
+                                torch.from_numpy(case["fromWorld"].reshape(B, 1, 4, 4)),
+                                torch.from_numpy(case["toWorld"].reshape(B, 1, 4, 4)), B,
+                                n_steps_each=2, step_lr=6.2e-6, existMask=torch.from_numpy(case["exist"]),
+                                denoise=True, verbose=False, grad_ref=1, correlation_coefficient=0.01)
+        # images = [newImages (last level, step 1), newImages (step 2), final x]  (KITTISampling.py:418-419, 511)
+        assert len(imgs) == 3
+        save(fname, new=imgs[0].numpy(), new2=imgs[1].numpy(), final=imgs[2].numpy())
 
 
 # AllForOne sampler loop end to end: (setting, minStepToShare).  Setting 5 ramps cc = (c+1)/L over

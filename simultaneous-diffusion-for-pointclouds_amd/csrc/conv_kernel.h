@@ -85,6 +85,31 @@ struct ConvTile {
 
 SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
+// The 16x16 3x3 tap schedule (bf16 modes): each of the NT taps of a chunk is 32 MFMA blocks, and the
+// tap's other work -- the next taps' weight loads, the A-fragment LDS reads, the next chunk's patch
+// transform and the chunk after next's LDS-DMA -- is dealt out to the blocks one small filler at a
+// time, so every block's VALU/LDS/VMEM issue fits beside its MFMAs (an MFMA leaves 8 of its 16
+// issue cycles to other instructions, MI355X_MICROARCH.md constants).  Staging unit k (16 B of one
+// patch pixel) is transformed in tap tap_of(k): the units spread over all taps, and each unit's next
+// DMA follows its own transform, so it has a whole chunk to land.
+template <int NU, int NT>
+struct XformPlan {
+  static constexpr int tap_of(int k) { return k * NT / NU; }
+  static constexpr int first(int tap) {
+    int k = 0;
+    while (k < NU && tap_of(k) < tap) ++k;
+    return k;
+  }
+  static constexpr int count(int tap) {
+    int n = 0;
+    for (int k = 0; k < NU; ++k) n += tap_of(k) == tap ? 1 : 0;
+    return n;
+  }
+  static constexpr int NSTG = 5;   // transform stages of one piece (2 channels of a unit)
+  // block of stage slot q of Q in a tap: blocks 2 .. 31, evenly
+  static constexpr int stage_blk(int q, int Q) { return 2 + q * 30 / (Q > 0 ? Q : 1); }
+};
+
 // SH: MFMA shape of the bf16 modes -- 32 = v_mfma_f32_32x32x16_bf16 (wave tile = 4 x 2 fragments
 // of 32 px x 32 Cout, two 16-deep k steps per 32-channel chunk), 16 = v_mfma_f32_16x16x32_bf16
 // (8 x 4 fragments of 16 px x 16 Cout, one 32-deep k step per chunk).  Same cycles per FLOP; the
@@ -117,6 +142,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
 #ifdef SDP_TIMING
   unsigned long long tclk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tbar = 0;
+  const unsigned long long rt0 = __builtin_amdgcn_s_memrealtime();   // 100 MHz: the in-kernel clock
 #endif
   SDP_T(0);
   const int wm = WM == 1 ? 0 : (wave & 1), wn = WM == 1 ? wave : (wave >> 1);
@@ -229,10 +255,13 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   // consumed only by the next chunk's transform, so the loads stay in flight across a chunk
   const float* ssb = a.pro_ss + (size_t)b * a.ss_bstride;
   const int my_cv = tid & 7;                        // every unit of a thread has cv == tid % 8
-  float4 ssv0, ssv1;                                // (scale, shift) of this thread's 4 channels
-  auto load_ss = [&](int chunk) __attribute__((always_inline)) {
-    ssv0 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
-    ssv1 = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
+  // (scale, shift) of this thread's 4 channels, double-buffered by chunk parity: chunk c's rows live
+  // in ssv[c & 1][0..1] (the transform of chunk c writes patch buffer c & 1 too)
+  float4 ssv[2][2];
+  auto load_ss = [&](auto buf, int chunk) __attribute__((always_inline)) {
+    constexpr int SB = decltype(buf)::value;
+    ssv[SB][0] = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
+    ssv[SB][1] = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
   };
 
   // Staging unit u = 16 B (4 channels) of one patch pixel.  Its byte offset inside the image
@@ -275,6 +304,18 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
         uoff[k], chunk * 128, 0, SDP_DMA_AUX);
   };
+  // the same DMA as inline asm (common.h dma16_lds_opaque), for the main loop of the 3x3 tap schedule:
+  // the compiler cannot tell the raw slots apart and would wait for every DMA in flight (vmcnt(0))
+  // before the next raw read.  Ordering without that wait: unit k's slot is read again one chunk
+  // later, and the weight loads issued after its DMA -- which complete in issue order with it --
+  // are waited for two taps later, before their MFMAs
+  const i32x4 irs_o = buffer_desc(inb, (uint32_t)(a.H * a.W * Cin * 4));
+  auto load_unit_o = [&](auto kc, int chunk) __attribute__((always_inline)) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (SDP_KO & 1) return;
+    const uint32_t base = (uint32_t)(uintptr_t)(raw + ((tid & ~63) + k * NTH) * 16);
+    dma16_lds_opaque(irs_o, base, uoff[k], chunk * 128);
+  };
   // transform staging unit k of raw into patch buffer PB
   // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
   auto xform_load = [&](auto kc) __attribute__((always_inline)) {
@@ -285,6 +326,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     constexpr int k = decltype(kc)::value;
     constexpr int PB = decltype(pb)::value;
     const int pix = (tid + k * NTH) >> 3;   // units past the patch land in its slack: no branch
+    const float4 ssv0 = ssv[PB][0], ssv1 = ssv[PB][1];
     v.x = fmaf(v.x, ssv0.x, ssv0.y);
     v.y = fmaf(v.y, ssv0.z, ssv0.w);
     v.z = fmaf(v.z, ssv1.x, ssv1.y);
@@ -319,7 +361,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     if constexpr (SDP_KO & 2) return;
     const int pix = (tid + k * NTH) >> 3;
     float x0 = h ? v4.z : v4.x, x1 = h ? v4.w : v4.y;
-    const float4 sv = h ? ssv1 : ssv0;
+    const float4 sv = ssv[PB][h];
     x0 = fmaf(x0, sv.x, sv.y);
     x1 = fmaf(x1, sv.z, sv.w);
     if constexpr (PELU) {
@@ -349,11 +391,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   // ---- prologue: chunk 0 staged + transformed, chunk 1 in flight ----
   load_b(std::integral_constant<int, 0>{}, 0, 0);
   static_for<1, NBUF - 1>([&](auto j) { load_b(j, 0, decltype(j)::value); });
-  load_ss(0);
+  load_ss(std::integral_constant<int, 0>{}, 0);
   static_for<0, NU>([&](auto k) { load_unit(k, 0); });
   static_for<0, NU>([&](auto k) { xform_unit(k, std::integral_constant<int, 0>{}); });
   if (nchunks > 1) {
-    load_ss(1);
+    load_ss(std::integral_constant<int, 1>{}, 1);
     static_for<0, NU>([&](auto k) { load_unit(k, 1); });
   }
   __syncthreads();
@@ -403,7 +445,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         });
       };
       auto dmas = [&]() __attribute__((always_inline)) {
-        if constexpr (tap == NT - 1) load_ss(min(chunk + 2, nchunks - 1));
+        if constexpr (tap == NT - 1) load_ss(std::integral_constant<int, P>{}, min(chunk + 2, nchunks - 1));
         static_for<0, NU>([&](auto kc) {
           constexpr int dt = NT > XT ? XT : 0;   // all at the first free tap: the longest flight
           if constexpr (dt == tap) load_unit(kc, chunk + 2);
@@ -504,10 +546,168 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     tbar += __builtin_amdgcn_s_memtime() - tb0;
 #endif
   };
+  // ---- the 16x16 3x3 tap schedule (XformPlan): 32 blocks of (s, nj, i) per tap, each 3 MFMAs
+  // (fp32x3) or 1 (bf16) plus at most a filler or two:
+  //   blocks 0 .. NQ-1       : the A fragments of this tap's half s = 1 (cb), one LDS read each
+  //   odd blocks 1 .. 2NQ-1  : the weight fragments of tap + 2 (ring slot (tap + 2) % 3), one load each
+  //   blocks 16 .. 16+NQ-1   : the half-0 fragments of tap + 1 (into ca: free after block 15)
+  //   blocks 0, 1            : the raw values of the units this tap transforms (XformPlan::tap_of)
+  //   blocks 2 .. 31         : their transform, 5 stages per 2-channel piece
+  //   blocks 30, 31          : the LDS-DMA of those units for the chunk after next (raw slot free)
+  using XP = XformPlan<NU, NT>;
+  constexpr int NQ = MODE == MODE_F32X3 ? 8 : 4;   // A reads per half tap = weight loads per tap
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  // one A fragment: pixel group i of half s of tap `tap`, hi (LO = 0) or lo part
+  auto read_a1 = [&](const char* pat, auto tap_c, auto s_c, auto i_c, auto lo_c) __attribute__((always_inline)) {
+    constexpr int tap = decltype(tap_c)::value, s = decltype(s_c)::value, i = decltype(i_c)::value;
+    constexpr int kh = tap / 3, kw = tap % 3, mb = 4 * s + i;
+    constexpr int mr = mb / (TC / 16), mc = (mb % (TC / 16)) * 16;
+    return *reinterpret_cast<const bf16x8*>(pat + ((wrow0 + mr + kh) * T::PC + mc + kw) * PSTRIDE + a_lane_off16 +
+                                            (decltype(lo_c)::value ? 64 : 0));
+  };
+  // weight load q of (chunk, tap) into ring slot J: q = 2 nj + part (fp32x3) or nj (bf16)
+  auto load_b1 = [&](auto buf, auto q_c, int chunk, int tap) __attribute__((always_inline)) {
+    constexpr int J = decltype(buf)::value, q = decltype(q_c)::value;
+    constexpr int nj = MODE == MODE_F32X3 ? (q >> 1) : q, part = MODE == MODE_F32X3 ? (q & 1) : 0;
+    if constexpr (SDP_KO & 4) return;
+    const int so = __builtin_amdgcn_readfirstlane(((chunk * NT + tap) * NB) * 4096 + (part ? wlo16 : 0));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj], so, 0);
+    bq[J][nj >> 1][2 * (nj & 1) + part] = make_uint4(v.x, v.y, v.z, v.w);
+  };
+  auto do_chunk9 = [&](auto parity, int chunk) __attribute__((always_inline)) {
+    constexpr int P = decltype(parity)::value;
+    const char* pat = lds + P * T::PATCH_BYTES;
+    bf16x8 ca[2][4], cb[2][4];   // [hi, lo][i]: half s = 0 / s = 1 of the current tap
+    static_for<0, 4>([&](auto i) {
+      ca[0][i] = read_a1(pat, I0{}, I0{}, i, I0{});
+      if constexpr (MODE == MODE_F32X3) ca[1][i] = read_a1(pat, I0{}, I0{}, i, I1{});
+    });
+    load_ss(std::integral_constant<int, P>{}, min(chunk + 2, nchunks - 1));   // buffer P: chunk-1's, free
+    static_for<0, NT>([&](auto tap_c) {
+      constexpr int tap = decltype(tap_c)::value;
+      constexpr int CUR = tap % 3, NXT = (tap + 2) % 3;
+      constexpr int U0 = XP::first(tap), UN = XP::count(tap), Q = UN * 2 * XP::NSTG;
+      constexpr int UNA = UN > 0 ? UN : 1;
+      const int wchunk = tap + 2 < NT ? chunk : min(chunk + 1, nchunks - 1);
+      constexpr int wtap = tap + 2 < NT ? tap + 2 : tap + 2 - NT;
+      float4 xr[UNA];                                  // raw values of this tap's units
+      float py0[2 * UNA], py1[2 * UNA], pe0[2 * UNA], pe1[2 * UNA];
+      uint32_t phi[2 * UNA], plo[2 * UNA];
+      // stage st of piece pc (unit U0 + pc / 2, channels 2 (pc % 2) ..): the xform_piece arithmetic,
+      // split so that each stage fits one block's free issue cycles
+      auto stage = [&](auto pc_c, auto st_c) __attribute__((always_inline)) {
+        constexpr int pc = decltype(pc_c)::value, st = decltype(st_c)::value;
+        constexpr int j = pc / 2, h = pc % 2, k = U0 + j, PB = 1 - P;
+        if constexpr (SDP_KO & 2) return;
+        if constexpr (st == 0) {
+          const float4 v = xr[j];
+          const float4 sv = ssv[PB][h];
+          py0[pc] = fmaf(h ? v.z : v.x, sv.x, sv.y);
+          py1[pc] = fmaf(h ? v.w : v.y, sv.z, sv.w);
+          if constexpr (PELU) {
+            pe0[pc] = fminf(py0[pc], 0.f);
+            pe1[pc] = fminf(py1[pc], 0.f);
+          }
+        } else if constexpr (st == 1) {
+          if constexpr (PELU) {
+            pe0[pc] = __expf(pe0[pc]);
+            pe1[pc] = __expf(pe1[pc]);
+          }
+        } else if constexpr (st == 2) {
+          if constexpr (PELU) {   // elu_max (common.h)
+            py0[pc] = fmaxf(py0[pc], pe0[pc] - 1.0f);
+            py1[pc] = fmaxf(py1[pc], pe1[pc] - 1.0f);
+          }
+          if constexpr (ZP) {
+            const bool ok = (uvalid >> k) & 1u;
+            py0[pc] = ok ? py0[pc] : 0.f;
+            py1[pc] = ok ? py1[pc] : 0.f;
+          }
+        } else if constexpr (st == 3) {
+          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+          bf16x2 hi;
+          hi[0] = (__bf16)py0[pc];
+          hi[1] = (__bf16)py1[pc];
+          phi[pc] = *reinterpret_cast<const uint32_t*>(&hi);
+          if constexpr (MODE == MODE_F32X3) {
+            bf16x2 lo;
+            lo[0] = (__bf16)(py0[pc] - (float)hi[0]);
+            lo[1] = (__bf16)(py1[pc] - (float)hi[1]);
+            plo[pc] = *reinterpret_cast<const uint32_t*>(&lo);
+          }
+        } else {
+          const int pix = (tid + k * NTH) >> 3;
+          char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 8 + h * 4;
+          *reinterpret_cast<uint32_t*>(dst) = phi[pc];
+          if constexpr (MODE == MODE_F32X3) *reinterpret_cast<uint32_t*>(dst + 64) = plo[pc];
+        }
+      };
+      static_for<0, 32>([&](auto blk_c) {
+        constexpr int blk = decltype(blk_c)::value;
+        constexpr int s = blk >> 4, nj = (blk >> 2) & 3, i = blk & 3, mb = 4 * s + i;
+        // ---- fillers that feed this tap: raw reads first (the transform waits on them)
+        if constexpr (blk < UN) xr[blk] = xform_load(std::integral_constant<int, U0 + blk>{});
+        // ---- the block's MFMAs
+        {
+          const uint4 h4 = bq[CUR][nj >> 1][2 * (nj & 1)], l4 = bq[CUR][nj >> 1][2 * (nj & 1) + 1];
+          const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
+          const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
+          const bf16x8 ahi = s == 0 ? ca[0][i] : cb[0][i];
+          if constexpr (TRANS) {   // D = W x X: rows = Cout, columns = pixels (same fragment registers)
+            if constexpr (MODE == MODE_F32X3) {
+              const bf16x8 alo = s == 0 ? ca[1][i] : cb[1][i];
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi, alo, acc4[mb][nj], 0, 0, 0);
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(blo, ahi, acc4[mb][nj], 0, 0, 0);
+            }
+            acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bhi, ahi, acc4[mb][nj], 0, 0, 0);
+          } else {
+            if constexpr (MODE == MODE_F32X3) {
+              const bf16x8 alo = s == 0 ? ca[1][i] : cb[1][i];
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bhi, acc4[mb][nj], 0, 0, 0);
+              acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, blo, acc4[mb][nj], 0, 0, 0);
+            }
+            acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc4[mb][nj], 0, 0, 0);
+          }
+        }
+        // ---- fillers for later taps
+        if constexpr (blk < NQ) {   // this tap's half-1 fragments (used from block 16)
+          constexpr int q = blk, ii = MODE == MODE_F32X3 ? (q >> 1) : q, lo = MODE == MODE_F32X3 ? (q & 1) : 0;
+          cb[lo][ii] = read_a1(pat, tap_c, I1{}, std::integral_constant<int, ii>{}, std::integral_constant<int, lo>{});
+        }
+        if constexpr ((blk & 1) && (blk >> 1) < NQ)   // tap + 2's weights
+          load_b1(std::integral_constant<int, NXT>{}, std::integral_constant<int, (blk >> 1)>{}, wchunk, wtap);
+        if constexpr (tap + 1 < NT && blk >= 16 && blk < 16 + NQ) {   // tap + 1's half-0 fragments
+          constexpr int q = blk - 16, ii = MODE == MODE_F32X3 ? (q >> 1) : q, lo = MODE == MODE_F32X3 ? (q & 1) : 0;
+          ca[lo][ii] = read_a1(pat, std::integral_constant<int, tap + 1>{}, I0{}, std::integral_constant<int, ii>{},
+                               std::integral_constant<int, lo>{});
+        }
+        static_for<0, Q>([&](auto q_c) {   // transform stages dealt to this block
+          constexpr int q = decltype(q_c)::value;
+          if constexpr (XP::stage_blk(q, Q) == blk)
+            stage(std::integral_constant<int, q / XP::NSTG>{}, std::integral_constant<int, q % XP::NSTG>{});
+        });
+        if constexpr (UN > 0 && blk >= 32 - UN)   // the DMA of a transformed unit (its raw slot was read)
+          load_unit_o(std::integral_constant<int, U0 + blk - (32 - UN)>{}, chunk + 2);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+    // patch[P] free for chunk+2's transform, patch[1-P] complete (see do_chunk)
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+    if constexpr (!(SDP_KO & 8)) __builtin_amdgcn_s_barrier();
+  };
   static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
-  for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
-    do_chunk(std::integral_constant<int, 0>{}, chunk);
-    do_chunk(std::integral_constant<int, 1>{}, chunk + 1);
+  if constexpr (MODE != MODE_F32 && NT == 9) {
+    static_assert(XP::count(0) <= 2 && XP::NSTG * 2 * 2 <= 30, "one filler slot per block");
+    for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
+      do_chunk9(std::integral_constant<int, 0>{}, chunk);
+      do_chunk9(std::integral_constant<int, 1>{}, chunk + 1);
+    }
+  } else {
+    for (int chunk = 0; chunk < nchunks; chunk += 2) {
+      do_chunk(std::integral_constant<int, 0>{}, chunk);
+      do_chunk(std::integral_constant<int, 1>{}, chunk + 1);
+    }
   }
 
   SDP_T(3);
@@ -1187,6 +1387,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   if (tid == 0) {
     unsigned long long* o = a.dbg + blockIdx.x * 8;
     o[0] = tclk[0]; o[1] = tclk[1]; o[2] = tclk[2]; o[3] = tclk[3]; o[4] = tclk[4]; o[5] = tbar;
+    o[6] = rt0; o[7] = __builtin_amdgcn_s_memrealtime();
   }
 #endif
 #endif

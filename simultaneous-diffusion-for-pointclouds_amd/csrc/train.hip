@@ -17,6 +17,8 @@
 // Workspace = forward tape + backward buffers, bump-allocated in a fixed order; a dry run of
 // the same code computes its size (sdp_net_train_workspace_size).
 #include <cmath>
+#include <set>
+#include <string>
 
 #include "net_internal.h"
 
@@ -53,6 +55,8 @@ struct TrainPlan {
   const size_t* bucket_end = nullptr;
   hipEvent_t const* bucket_ev = nullptr;
   size_t done_prefix = 0;             // floats of the arena prefix whose gradients are final
+  std::set<std::string> done_keys;    // parameters whose gradients are final
+  size_t layout_pos = 0;              // net->layout entries [0, layout_pos) are all in done_keys
   size_t fwd_bytes = 0;
   size_t ws_need = 0;                 // forward + backward bytes (dry run), 0 = unknown
 
@@ -83,15 +87,22 @@ struct TrainPlan {
     return it->second;
   }
   int ks_of(const std::string& wkey) const { return (int)net->host.at(wkey + ".weight").shape[2]; }
-  // the gradients of `keys` are final once the launches enqueued so far have run
+  // the gradients of `keys` are final once the launches enqueued so far have run.  The final prefix
+  // advances only over layout entries that are ALL finished, in arena order: a parameter finished
+  // out of layout order (e.g. a key-ordered fallback layout) never lets a bucket event fire over a
+  // gradient that is still being written.  Invariant the bucket reducer relies on
+  // (sdp/gradreduce.py): no launch writes a parameter's gradient range after finished() named it.
   void finished(std::initializer_list<std::string> keys) {
     for (const auto& k : keys) {
       grad_order.push_back(k);
-      if (dry || !n_buckets) continue;
-      for (const auto& e : net->layout)
-        if (e.key == k) done_prefix = std::max(done_prefix, e.offset + (e.numel + 63) / 64 * 64);
+      done_keys.insert(k);
     }
     if (dry) return;
+    const auto& lay = net->layout;
+    while (layout_pos < lay.size() && done_keys.count(lay[layout_pos].key)) {
+      done_prefix = std::max(done_prefix, lay[layout_pos].offset + (lay[layout_pos].numel + 63) / 64 * 64);
+      ++layout_pos;
+    }
     while (next_bucket < n_buckets && done_prefix >= bucket_end[next_bucket])
       ok(hipEventRecord(bucket_ev[next_bucket++], st), "hipEventRecord (gradient bucket)");
   }
@@ -470,6 +481,8 @@ struct TrainPlan {
     grad_order.clear();
     next_bucket = 0;
     done_prefix = 0;
+    done_keys.clear();
+    layout_pos = 0;
     // scratch (upper bounds over every layer of the network)
     wpart_n = (size_t)(WGRAD_TARGET_BLOCKS + 64) * 9 * 128 * 32;   // >= splits x 9 x Cin x Cout for every conv
     wpart = take(wpart_n);

@@ -9,9 +9,14 @@ sdp_net_param_info) is averaged over the ranks with RCCL all-reduces:
   the backward finishes the gradients (sdp_net_finalize), so bucket i is final as soon as the
   backward has passed its last layer; ``sdp_net_backward_buckets`` records a HIP event there;
 * per bucket, a communication stream waits for that event, casts the bucket to the wire dtype
-  (bf16 by default for bf16 training: 59.4 MB on the wire for 29.7 M parameters instead of
-  118.8 MB fp32), all-reduces it (SUM) and writes the average back into the fp32 arena.  The
-  all-reduces of the early buckets run while the backward computes the later layers;
+  (fp32 by default, the reference's reduce; bf16 on request: 59.4 MB on the wire for 29.7 M
+  parameters instead of 118.8 MB, but a ring SUM in bf16 rounds the running sum at every hop),
+  all-reduces it (SUM) and writes the average back into the fp32 arena.  The all-reduces of the
+  early buckets run while the backward computes the later layers;
+* invariant (train.hip TrainPlan::finished): no backward launch writes a parameter's gradient range
+  after the bucket event that covers it, so the communication stream may read and rewrite a
+  bucket while the backward runs on.  tests/test_gpu_training.py checks it by poisoning every
+  finished bucket on the side stream and comparing the final gradients;
 * the optimizer step waits for the communication stream (the fp32 arena stays the master copy:
   only the wire carries bf16).
 
@@ -21,7 +26,7 @@ from __future__ import annotations
 
 import torch
 
-DEFAULT_BUCKET_FLOATS = 8 << 20     # 8 M parameters = 16 MB of bf16 per all-reduce
+DEFAULT_BUCKET_FLOATS = 8 << 20     # 8 M parameters = 32 MB of fp32 per all-reduce
 
 
 def bucket_ends(layout, arena_floats: int, bucket_floats: int = DEFAULT_BUCKET_FLOATS):
@@ -41,7 +46,7 @@ class BucketedGradReducer:
     """Averages ``grads`` (flat fp32, the parameter arena layout) over the ranks of ``group``."""
 
     def __init__(self, grads: torch.Tensor, layout, group=None, bucket_floats: int = DEFAULT_BUCKET_FLOATS,
-                 wire_dtype: torch.dtype = torch.bfloat16):
+                 wire_dtype: torch.dtype = torch.float32):
         import torch.distributed as dist
         self.dist = dist
         self.group = group

@@ -52,8 +52,10 @@ class Trainer:
         self.weight_decay, self.amsgrad, self.alpha, self.momentum = float(weight_decay), bool(amsgrad), alpha, momentum
         self.ema, self.ema_mu = ema, ema_mu
         self.dist_group = dist_group
-        # gradient all-reduce on the wire: bf16 for bf16 training (59.4 MB), fp32 for fp32x3
-        self.grad_wire_dtype = grad_wire_dtype or (torch.bfloat16 if net.precision == "bf16" else torch.float32)
+        # gradient all-reduce on the wire: fp32 by default, as the reference's DataParallel reduce
+        # (an RCCL ring SUM in bf16 rounds the running sum at every hop, up to world-1 times);
+        # grad_wire_dtype=torch.bfloat16 halves the bytes (59.4 MB) at that cost
+        self.grad_wire_dtype = grad_wire_dtype or torch.float32
         self.bucket_floats = bucket_floats
         self._reducer = None
         n = _lib.SZ()
@@ -85,8 +87,12 @@ class Trainer:
 
     # ------------------------------------------------------------------ parameter views
     def named_parameters(self, arena: torch.Tensor | None = None):
+        """(key, view) in the reference module's registration order (param_shapes), wherever the
+        arena keeps the parameter: checkpoints keep the reference's key order."""
         a = self.params if arena is None else arena
-        for k, off, numel in self.layout:
+        where = {k: (off, numel) for k, off, numel in self.layout}
+        for k in self.shapes:
+            off, numel = where[k]
             yield k, a[off:off + numel].view(self.shapes[k])
 
     def named_grads(self):

@@ -262,13 +262,16 @@ def test_kitti_merge_matches_reference_golden(case_def):
     assert np.mean((new != 0) != (f["new"] != 0)) <= 1e-4
 
 
-@pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5)])
+@pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5), ("a_b7_s05_set8", 8)])
 def test_allforone_merge_matches_reference_golden(tag, setting):
+    """Settings 5 (cc ramp), 7 (controlled average) and 8 (controlled, allowance 5:
+    models/__init__.py:469-470)."""
     from sdp.merge import allforone_origins
     case = GI.merge_case(tag, 7, 64, 256)
     f = _g(f"merge_{tag}.npz")
     cc = 1.0 if setting == 5 else 0.01
-    new, xc = _gpu_merge(case, 7, 0.5, setting, 10, cc, origins=allforone_origins(CIRCLE_MODS))
+    allowance = 5 if setting >= 8 else 10
+    new, xc = _gpu_merge(case, 7, 0.5, setting, allowance, cc, origins=allforone_origins(CIRCLE_MODS))
     assert _close_frac(new, f["new"]) <= 1e-4
     assert _close_frac(_final_dc(xc, case), f["x"]) <= 1e-4
 
@@ -348,18 +351,22 @@ def test_config1_baseline_sampler_matches_golden(net256):
         assert np.abs(got - f[k]).max() <= 1e-4 * np.abs(f[k]).max(), k
 
 
-def test_kitti_sampler_end_to_end_matches_golden(net256):
+@pytest.mark.parametrize("tag,setting,fname", [("e2e", 5, "kitti_e2e_b2_64x256.npz"),
+                                                ("e2e_set7", 7, "kitti_e2e_set7_b2_64x256.npz")])
+def test_kitti_sampler_end_to_end_matches_golden(net256, tag, setting, fname):
+    """The kitti loop vs the reference-generated golden; setting 7 pins the cc ramp
+    (KITTISampling.py:106-109, sdp/sampling.py ramp)."""
     from sdp.sampling import anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti as samp
     from sdp.weights import get_sigmas_np
-    f = _g("kitti_e2e_b2_64x256.npz")
-    case = GI.merge_case("e2e", 2, 64, 256)
-    x0 = torch.from_numpy(GI.scorenet_input("e2e", 2, 64, 256)).to(DEV)
+    f = _g(fname)
+    case = GI.merge_case(tag, 2, 64, 256)
+    x0 = torch.from_numpy(GI.scorenet_input(tag, 2, 64, 256)).to(DEV)
     t = lambda a: torch.from_numpy(a).to(DEV)
-    images, _, _ = samp(x0, t(case["ref"]), t(case["mask"]), t(case["sky"]), None, 2, 5, 10, net256,
+    images, _, _ = samp(x0, t(case["ref"]), t(case["mask"]), t(case["sky"]), None, 2, setting, 10, net256,
                         get_sigmas_np()[229:232], t(case["fromWorld"].reshape(2, 1, 4, 4)),
                         t(case["toWorld"].reshape(2, 1, 4, 4)), 2, n_steps_each=2, step_lr=6.2e-6,
                         existMask=t(case["exist"]), denoise=True, verbose=False, grad_ref=1,
-                        correlation_coefficient=0.01, noise_fn=_noise_feed("e2e"))
+                        correlation_coefficient=0.01, noise_fn=_noise_feed(tag))
     assert len(images) == 3
     for got, want in ((images[0].numpy(), f["new"]), (images[1].numpy(), f["new2"]), (images[2].numpy(), f["final"])):
         assert _close_frac(got, want, rtol=1e-4, atol=1e-4 * np.abs(want).max()) <= 1e-3

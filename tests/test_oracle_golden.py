@@ -121,7 +121,7 @@ def test_identity_pose_row_shift():
     assert (new[:, 0, 1:] != 0).mean() > 0.5
 
 
-@pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5)])
+@pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5), ("a_b7_s05_set8", 8)])
 def test_allforone_merge_oracle_matches_reference(tag, setting):
     case = GI.merge_case(tag, 7, 64, 256)
     f = _g(f"merge_{tag}.npz")
@@ -186,13 +186,17 @@ def test_config1_baseline_sampler(params128):
         np.testing.assert_allclose(imgs[i], f[k], rtol=1e-5, atol=1e-5, err_msg=k)
 
 
-def test_kitti_sampler_end_to_end(params128):
-    f = _g("kitti_e2e_b2_64x256.npz")
-    case = GI.merge_case("e2e", 2, 64, 256)
-    x0 = GI.scorenet_input("e2e", 2, 64, 256)
-    images, _, _ = S.sampler_kitti(x0, case["ref"], case["mask"], case["sky"], 2, 5, 10, _score_fn(params128),
+@pytest.mark.parametrize("tag,setting,fname", [("e2e", 5, "kitti_e2e_b2_64x256.npz"),
+                                                ("e2e_set7", 7, "kitti_e2e_set7_b2_64x256.npz")])
+def test_kitti_sampler_end_to_end(params128, tag, setting, fname):
+    """oracle sampler_kitti == the reference kitti loop; setting 7 pins the cc ramp
+    (KITTISampling.py:106-109)."""
+    f = _g(fname)
+    case = GI.merge_case(tag, 2, 64, 256)
+    x0 = GI.scorenet_input(tag, 2, 64, 256)
+    images, _, _ = S.sampler_kitti(x0, case["ref"], case["mask"], case["sky"], 2, setting, 10, _score_fn(params128),
                                    get_sigmas_np()[229:232], case["fromWorld"], case["toWorld"], 2, 2, 6.2e-6,
-                                   case["exist"], _noise_feed("e2e"))
+                                   case["exist"], _noise_feed(tag))
     assert len(images) == 3
     np.testing.assert_allclose(images[0], f["new"], rtol=1e-5, atol=1e-5)
     np.testing.assert_allclose(images[1], f["new2"], rtol=1e-5, atol=1e-5)

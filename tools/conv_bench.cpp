@@ -90,17 +90,19 @@ int main(int argc, char** argv) {
 #ifdef SDP_TIMING
   std::vector<unsigned long long> d((size_t)nwg_max * 8);
   CK(hipMemcpy(d.data(), dbg, d.size() * 8, hipMemcpyDeviceToHost));
-  double s[6] = {0}; int n = 0; unsigned long long tmin = ~0ull, tmax = 0;
+  double s[7] = {0}; int n = 0; unsigned long long tmin = ~0ull, tmax = 0;
   for (int i = 0; i < nwg_max; ++i) {
     const unsigned long long* o = &d[(size_t)i * 8];
     if (!o[0]) continue;
     ++n;
     s[0] += o[1] - o[0]; s[1] += o[2] - o[1]; s[2] += o[3] - o[2]; s[3] += o[4] - o[3]; s[4] += o[5];
     s[5] += o[4] - o[0];
+    s[6] += (double)(o[4] - o[0]) / (double)(o[7] > o[6] ? o[7] - o[6] : 1) * 0.1;   // GHz: memtime / memrealtime (100 MHz)
     tmin = std::min(tmin, o[0]); tmax = std::max(tmax, o[4]);
   }
   printf("  per-WG memtime ticks (n=%d): setup %.0f  prologue %.0f  loop %.0f (barrier %.0f)  epilogue %.0f  total %.0f ; "
-         "span of last launch %llu\n", n, s[0] / n, s[1] / n, s[2] / n, s[4] / n, s[3] / n, s[5] / n, tmax - tmin);
+         "span of last launch %llu ; in-kernel clock %.3f GHz\n", n, s[0] / n, s[1] / n, s[2] / n, s[4] / n, s[3] / n,
+         s[5] / n, tmax - tmin, s[6] / n);
 #endif
   return 0;
 }
