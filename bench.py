@@ -177,6 +177,27 @@ def pmc_traffic(precision, V, cls):
     return None, None
 
 
+def conv_clock(cls):
+    """Clock the chip held and MFMA-busy fraction of conv class `cls` in this network, from the committed
+    PMC + in-kernel-clock passes (tools/conv_clock.sh -> profiles/rNN_conv_clock.json, newest first),
+    keyed like pmc_traffic by the conv source hash: None when no file matches the current tree."""
+    import glob
+    from sdp import _build
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_conv_clock.json")), reverse=True):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if not isinstance(d, dict) or d.get("conv_source_hash") != _build.conv_source_hash():
+            continue
+        for r in d.get("classes", []):
+            if r.get("class") == cls and "clock_GHz" in r:
+                return {"clock_GHz": r["clock_GHz"], "mfma_busy_frac": r["mfma_busy_frac"],
+                        "source": f"{os.path.basename(fn)} (conv source {d['conv_source_hash'][:12]})"}
+    return None
+
+
 # ----------------------------------------------------------------------------- timing harness
 def timed(step, args, dist, dev):
     for i in range(args.warmup):
@@ -330,12 +351,18 @@ def run_sampling(args, rank, N, dist, dev):
                     "frac": round(merge_bytes / (merge_us * 1e-6) / 1e9 / HBM_PEAK, 4),
                     "bytes_basis": "SURVEY 8(d): 7.3 MB per view; latency/atomic-bound, not HBM-bound"})
         traffic, tsrc = pmc_traffic(prec, V, cls) if args.workload == "line" else (None, None)
+        clk = conv_clock(cls) if (args.workload == "line" and prec == "fp32x3") else None
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": round(PEAK[prec], 1),
                 "unit": "TFLOP/s", "frac": round(achieved / PEAK[prec], 4),
                 "traffic": traffic, "traffic_source": tsrc,
                 "algorithmic_bytes": 2 * V * 32 * 512 * 256 * 4 + 256 * 256 * 9 * (2 if prec == "bf16" else 4),
                 "kernel": f"conv_mfma_kernel [{cls}]", "avg_launch_us": round(avg_s * 1e6, 2),
                 "flops_per_launch": fl, "conv_ms_per_step": round(conv_ms, 3), "memory_bound": mem}
+        if clk is not None:
+            # the peak at the clock the chip held under this load (power-limited DVFS), this run's time
+            roof.update(clock_GHz=clk["clock_GHz"], mfma_busy_frac=clk["mfma_busy_frac"],
+                        frac_at_clock=round(achieved / (PEAK[prec] * clk["clock_GHz"] / 2.4), 4),
+                        clock_source=clk["source"])
         return dt, roof
 
     net_box = [net]
