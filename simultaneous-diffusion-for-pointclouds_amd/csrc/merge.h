@@ -5,7 +5,7 @@
 namespace sdp {
 
 struct MergeGeom {
-  double hA, vA, hMin, bigMin;
+  double hA, vA, hMin, bigMin, vMin;
   int H, W, big;
 };
 
@@ -17,8 +17,9 @@ struct MergeArgs {
   const uint8_t* exist;    // [aB][HW]
   const uint8_t* sky;      // [n_src][HW]
   const int32_t* refmask;  // [n_src][2][HW]
-  const double* trig;      // cos_az[W], sin_az[W], cos_el[H], sin_el[H]
   double4* world;          // [n_src][HW] world point + source-valid flag
+  float* isnap;            // [n_src][HW] the sources' intensity channel before the correction (resolve's
+                           //   nearest-point intensity reads it while the fused pass corrects x in place)
   // per-cell results [n_out][cells] (cells = big x W), written once per cell by merge_tile
   uint32_t* cnt;
   double* sumL;
@@ -28,13 +29,13 @@ struct MergeArgs {
   // binning of the (output view, source point) pairs by destination tile = (output view, big
   // row): per-chunk tile counts [T][nchunk] -> exclusive offsets (tile-major), and the records
   uint32_t* tcount;        // [T][nchunk], scanned in place
-  uint32_t* bsum;          // scan block totals
+  uint32_t* bsum;          // scan block totals -> their exclusive scan (+ the grand total at [nb])
+  uint32_t* toff;          // [T + 1] first record of every tile (+ the total): the segment passes' table
   float4* rec;             // [pairs]: (code as 2 floats' bits, intensity, s << 10 | column)
   int32_t* pcell;          // [pairs]: K1's projection of every pair (big-grid cell or -1) and its
   double* pcode;           //   depth code, so K3 scatters without projecting again (same bits)
   int nchunk;
   float* newimg;           // [n_out][2][HW]
-  uint8_t* maskimg;        // [n_out][HW]
   const uint32_t* absmax;  // max |x[:,0]| bits over all views
   float* xout;             // x_all (corrected in place for the output views)
   MergeGeom g;

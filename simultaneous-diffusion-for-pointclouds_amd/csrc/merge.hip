@@ -23,19 +23,35 @@
 namespace sdp {
 
 // ---------------------------------------------------------------- K0: source points -> world
+// Also (one launch instead of four): the cos/sin of the point's column azimuth and row elevation
+// (KITTISampling.py:101-102, float64), the output views' grids reset (counts and sums 0, nearest code
+// and index all-ones) and the snapshot of the sources' intensities that the fused resolve+apply pass
+// reads while it corrects x in place.
 __global__ __launch_bounds__(256) void merge_world_kernel(MergeArgs a) {
-  const int HW = a.g.H * a.g.W;
+  const int H = a.g.H, W = a.g.W, HW = H * W;
   const size_t n = (size_t)a.n_src * HW;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+  const size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  const size_t ncell = (size_t)a.n_out * a.g.big * W;
+  for (size_t c = i0; c < ncell; c += stride) {
+    a.cnt[c] = 0u;
+    a.sumL[c] = 0.0;
+    a.sumI[c] = 0.0;
+    a.minkey[c] = ~0ull;
+    a.minidx[c] = ~0u;
+  }
+  for (size_t i = i0; i < n; i += stride) {
     const int v = i / HW, p = i % HW;
-    const int r = p / a.g.W, c = p % a.g.W;
+    const int r = p / W, c = p % W;
     const float x0 = a.x[(size_t)v * 2 * HW + p];
+    a.isnap[i] = a.x[(size_t)v * 2 * HW + HW + p];
     // realDistance = (2^(|x|*6/smod) - 1) * (+-1), float32 (KITTISampling.py:164-166)
     const float e = __fdiv_rn(__fmul_rn(fabsf(x0), 6.0f), a.smod);
     float rd = __fsub_rn(exp2f(e), 1.0f);
     if (x0 < 0.f) rd = -rd;
-    const double cz = a.trig[c], sz = a.trig[a.g.W + c];
-    const double ce = a.trig[2 * a.g.W + r], se = a.trig[2 * a.g.W + a.g.H + r];
+    const double az = (double)(W - 1 - c) * a.g.hA + a.g.hMin;
+    const double el = (double)(H - 1 - r) * a.g.vA + a.g.vMin;
+    const double cz = cos(az), sz = sin(az);
+    const double ce = cos(el), se = sin(el);
     const double rdd = (double)rd;
     double px = __dmul_rn(__dmul_rn(rdd, cz), ce);
     double py = __dmul_rn(__dmul_rn(rdd, sz), ce);
@@ -168,18 +184,50 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
   for (int t = threadIdx.x; t < T; t += 256) a.tcount[(size_t)t * a.nchunk + blockIdx.x] = hist[t];
 }
 
-__global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, size_t per_chunk) {
-  extern __shared__ uint32_t cur[];
-  const int HW = a.g.H * a.g.W, T = a.n_out * a.g.big;
-  constexpr int SB = 2048;   // scan block (see scan kernels)
-  for (int t = threadIdx.x; t < T; t += 256) {
+// The top level of the offset scan rides here (one launch less): every workgroup scans the nb block
+// totals of merge_scan_block_kernel in LDS; workgroup 0 also publishes every tile's first record and
+// the total (toff) for the segment passes, which run after this launch.
+__global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, size_t per_chunk, int nb) {
+  extern __shared__ uint32_t cur[];                // [T] tile cursors, then [nb + 1] scanned block totals
+  const int HW = a.g.H * a.g.W, T = a.n_out * a.g.big, tid = threadIdx.x;
+  uint32_t* sb = cur + T;
+  constexpr int SB = 2048;   // scan block (merge_scan_block_kernel)
+  {
+    __shared__ uint32_t part[256];
+    const int per = (nb + 255) / 256, b0 = tid * per;
+    uint32_t t = 0;
+    for (int k = 0; k < per; ++k) t += b0 + k < nb ? a.bsum[b0 + k] : 0u;
+    part[tid] = t;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      const uint32_t y = tid >= off ? part[tid - off] : 0u;
+      __syncthreads();
+      part[tid] += y;
+      __syncthreads();
+    }
+    uint32_t run = part[tid] - t;
+    for (int k = 0; k < per; ++k)
+      if (b0 + k < nb) {
+        const uint32_t x = a.bsum[b0 + k];
+        sb[b0 + k] = run;
+        run += x;
+      }
+    if (tid == 255) sb[nb] = part[255];
+    __syncthreads();
+  }
+  for (int t = tid; t < T; t += 256) {
     const size_t k = (size_t)t * a.nchunk + blockIdx.x;
-    cur[t] = a.tcount[k] + a.bsum[k / SB];
+    cur[t] = a.tcount[k] + sb[k / SB];
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {   // chunk 0's cursors are the tiles' first records
+    for (int t = tid; t < T; t += 256) a.toff[t] = cur[t];
+    if (tid == 0) a.toff[T] = sb[nb];
   }
   __syncthreads();
   const size_t n = (size_t)a.n_out * a.aB * HW;
   const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
-  for (size_t i = i0 + threadIdx.x; i < i1; i += 256) {
+  for (size_t i = i0 + tid; i < i1; i += 256) {
     const int cell = a.pcell[i];
     if (cell < 0) continue;
     int ol, s, o, m0;
@@ -196,8 +244,8 @@ __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, siz
   }
 }
 
-// exclusive scan of v[0..n) in blocks of 2048 (block totals -> bsum), then of the totals
-// (grand total -> bsum[nb]); consumers add bsum[k / 2048] to v[k]
+// exclusive scan of v[0..n) in blocks of 2048 (block totals -> bsum; their scan is done by the
+// consumer, merge_bin_scatter_kernel); consumers add the scanned bsum[k / 2048] to v[k]
 __global__ __launch_bounds__(256) void merge_scan_block_kernel(uint32_t* __restrict__ v, size_t n,
                                                                uint32_t* __restrict__ bsum) {
   __shared__ uint32_t sh[256];
@@ -226,68 +274,46 @@ __global__ __launch_bounds__(256) void merge_scan_block_kernel(uint32_t* __restr
   if (tid == 255) bsum[blockIdx.x] = sh[255];
 }
 
-__global__ __launch_bounds__(1024) void merge_scan_top_kernel(uint32_t* __restrict__ bsum, int nb) {
-  __shared__ uint32_t sh[1024];
-  const int tid = threadIdx.x, per = (nb + 1023) / 1024;
-  const int b0 = tid * per;
-  uint32_t t = 0;
-  for (int k = 0; k < per; ++k) t += b0 + k < nb ? bsum[b0 + k] : 0u;
-  sh[tid] = t;
-  __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {
-    const uint32_t y = tid >= off ? sh[tid - off] : 0u;
-    __syncthreads();
-    sh[tid] += y;
-    __syncthreads();
-  }
-  uint32_t run = sh[tid] - t;
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < nb) {
-      const uint32_t x = bsum[b0 + k];
-      bsum[b0 + k] = run;
-      run += x;
-    }
-  if (tid == 1023) bsum[nb] = sh[1023];
-}
-
-// record range of tile t: [tile_off(t), tile_off(t + 1)), the last one ending at the total
-__device__ __forceinline__ uint32_t tile_off(const MergeArgs& a, int t, int T, int nb) {
-  if (t >= T) return a.bsum[nb];
-  const size_t k = (size_t)t * a.nchunk;
-  return a.tcount[k] + a.bsum[k / 2048];
-}
-// the tile whose range holds record j (largest t with tile_off(t) <= j)
-__device__ __forceinline__ int tile_of(const MergeArgs& a, uint32_t j, int T, int nb) {
+// the tile whose range holds record j (largest t with toff[t] <= j), on the LDS copy of the table
+__device__ __forceinline__ int tile_of(const uint32_t* toff, uint32_t j, int T) {
   int lo = 0, hi = T - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (tile_off(a, mid, T, nb) <= j) lo = mid;
+    if (toff[mid] <= j) lo = mid;
     else hi = mid - 1;
   }
   return lo;
+}
+// the tile table [T + 1] into LDS (dynamic shared memory after the kernel's static arrays)
+__device__ __forceinline__ void load_toff(const MergeArgs& a, uint32_t* st, int T) {
+  for (int t = threadIdx.x; t <= T; t += 256) st[t] = a.toff[t];
 }
 
 // K4a: a workgroup sums MERGE_SEG consecutive records (tile-sorted) in LDS over the first two
 // tiles they touch (records of further tiles, a sparse stretch, go straight to global
 // atomics) and adds its cells to the grids: one atomic per touched cell, contiguous lanes.
+// The tile of a record comes from the tile table in LDS (one global binary search per record of a
+// sparse stretch before: a chain of dependent L2 loads).
 constexpr int MERGE_SEG = 4096;
-__global__ __launch_bounds__(256) void merge_seg_sum_kernel(MergeArgs a, int nb) {
+__global__ __launch_bounds__(256) void merge_seg_sum_kernel(MergeArgs a) {
   __shared__ uint32_t scnt[2048];
   __shared__ double ssl[2048], ssi[2048];
   __shared__ unsigned long long smk[2048];
+  extern __shared__ uint32_t stoff[];
   const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big, big = a.g.big;
-  const uint32_t total = a.bsum[nb];
-  const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
-  if (j0 >= total) return;
+  load_toff(a, stoff, T);
   for (int c = tid; c < 2 * W; c += 256) {
     scnt[c] = 0u;
     ssl[c] = 0.0;
     ssi[c] = 0.0;
     smk[c] = ~0ull;
   }
-  const int t0 = tile_of(a, j0, T, nb);
-  const uint32_t e1 = tile_off(a, t0 + 1, T, nb), e2 = tile_off(a, t0 + 2, T, nb);
   __syncthreads();
+  const uint32_t total = stoff[T];
+  const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
+  if (j0 >= total) return;
+  const int t0 = tile_of(stoff, j0, T);
+  const uint32_t e1 = stoff[min(t0 + 1, T)], e2 = stoff[min(t0 + 2, T)];
   for (uint32_t j = j0 + tid; j < j1; j += 256) {
     const float4 r = a.rec[j];
     const unsigned long long cb =
@@ -301,7 +327,7 @@ __global__ __launch_bounds__(256) void merge_seg_sum_kernel(MergeArgs a, int nb)
       atomicAdd(&ssi[c], (double)r.z);
       atomicMin(&smk[c], cb);
     } else {
-      const int t = tile_of(a, j, T, nb);
+      const int t = tile_of(stoff, j, T);
       const size_t ci = ((size_t)(t / big) * big + t % big) * W + col;
       atomicAdd(&a.cnt[ci], 1u);
       atomicAdd(&a.sumL[ci], code);
@@ -322,23 +348,25 @@ __global__ __launch_bounds__(256) void merge_seg_sum_kernel(MergeArgs a, int nb)
 }
 
 // K4b: the lowest source index among the records whose code equals the cell's nearest code
-__global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a, int nb) {
+__global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a) {
   __shared__ uint32_t sidx[2048];
+  extern __shared__ uint32_t stoff[];
   const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big;
-  const uint32_t total = a.bsum[nb];
+  load_toff(a, stoff, T);
+  for (int c = tid; c < 2 * W; c += 256) sidx[c] = 0xffffffffu;
+  __syncthreads();
+  const uint32_t total = stoff[T];
   const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
   if (j0 >= total) return;
-  for (int c = tid; c < 2 * W; c += 256) sidx[c] = 0xffffffffu;
-  const int t0 = tile_of(a, j0, T, nb);
-  const uint32_t e1 = tile_off(a, t0 + 1, T, nb), e2 = tile_off(a, t0 + 2, T, nb);
-  __syncthreads();
+  const int t0 = tile_of(stoff, j0, T);
+  const uint32_t e1 = stoff[min(t0 + 1, T)], e2 = stoff[min(t0 + 2, T)];
   for (uint32_t j = j0 + tid; j < j1; j += 256) {
     const float4 r = a.rec[j];
     const unsigned long long cb =
         (unsigned long long)__float_as_uint(r.x) | ((unsigned long long)__float_as_uint(r.y) << 32);
     const uint32_t w = __float_as_uint(r.w);
     const int col = w & 1023u;
-    const int t = j < e2 ? (j < e1 ? t0 : t0 + 1) : tile_of(a, j, T, nb);
+    const int t = j < e2 ? (j < e1 ? t0 : t0 + 1) : tile_of(stoff, j, T);
     const size_t ci = (size_t)t * W + col;
     if (cb != a.minkey[ci]) continue;
     if (j < e2) atomicMin(&sidx[(j < e1 ? 0 : W) + col], w >> 10);
@@ -352,17 +380,26 @@ __global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a, int 
   }
 }
 
-// ---------------------------------------------------------------- K3: resolve cells -> new image
-__global__ __launch_bounds__(256) void merge_resolve_kernel(MergeArgs a) {
+// ---------------------------------------------------------------- K5: resolve cells -> new image, apply
+// One pass per output pixel (the resolve and the correction were two launches): the cell the pixel
+// reads (flip/roll for negative depth), the controlled average (KITTISampling.py:300-420), the new
+// image, then -- unless tooHigh (KITTISampling.py:162) -- x += cc * -(x - new) on the unknown pixels
+// of both channels.  The nearest point's intensity comes from the snapshot taken before any pixel is
+// corrected; a pixel's own depth sign is read before the pass writes it.
+__global__ __launch_bounds__(256) void merge_resolve_apply_kernel(MergeArgs a) {
   const int H = a.g.H, W = a.g.W, HW = H * W;
   const int cells = a.g.big * W;
   const size_t n = (size_t)a.n_out * HW;
+  const float mx = __uint_as_float(*a.absmax);
+  const bool too_high = __fdiv_rn(__fmul_rn(mx, 6.0f), a.smod) > 50.0f;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const int ol = i / HW, p = i % HW;
     const int r = p / W, c = p % W;
     const int o = a.o_begin + ol;
     const int m0 = (o / a.aB) * a.aB;
-    const bool neg = a.x[(size_t)o * 2 * HW + p] < 0.f;
+    const size_t x0i = (size_t)o * 2 * HW + p;
+    const float xd = a.x[x0i];
+    const bool neg = xd < 0.f;
     const int brow = neg ? (H - 1 - r) : (r + a.g.big - H);
     const int bcol = neg ? ((c - W / 2) % W + W) % W : c;
     const size_t ci = (size_t)ol * cells + brow * W + bcol;
@@ -378,7 +415,7 @@ __global__ __launch_bounds__(256) void merge_resolve_kernel(MergeArgs a) {
         const double lmin = __longlong_as_double((long long)a.minkey[ci]);
         const uint32_t s = a.minidx[ci];
         const int vl = s / HW, ps = s % HW;
-        const float Imin = a.x[((size_t)(m0 + vl) * 2 + 1) * HW + ps];
+        const float Imin = a.isnap[(size_t)(m0 + vl) * HW + ps];
         const double sm = (double)a.smod;
         const double A = exp2(__dmul_rn(fabs(Abar), 6.0) / sm) - 1.0;
         const double M = exp2(__dmul_rn(fabs(lmin), 6.0) / sm) - 1.0;
@@ -394,32 +431,15 @@ __global__ __launch_bounds__(256) void merge_resolve_kernel(MergeArgs a) {
     }
     const float depth = (float)(neg ? -code : code);
     const bool m = nn > 0 && a.exist[p] && a.sky[(size_t)o * HW + p];
-    if (a.newimg) {
-      a.newimg[((size_t)ol * 2 + 0) * HW + p] = depth;
-      a.newimg[((size_t)ol * 2 + 1) * HW + p] = inten;
+    a.newimg[((size_t)ol * 2 + 0) * HW + p] = depth;
+    a.newimg[((size_t)ol * 2 + 1) * HW + p] = inten;
+    if (too_high || !m) continue;
+    // KITTISampling.py:470-490: x += cc * -(x - new) where the reference mask is 0
+    if (a.refmask[x0i] == 0) a.xout[x0i] = __fadd_rn(xd, __fmul_rn(a.cc, -__fsub_rn(xd, depth)));
+    if (a.refmask[x0i + HW] == 0) {
+      const float xi = a.xout[x0i + HW];
+      a.xout[x0i + HW] = __fadd_rn(xi, __fmul_rn(a.cc, -__fsub_rn(xi, inten)));
     }
-    a.maskimg[i] = m ? 1 : 0;
-  }
-}
-
-// ---------------------------------------------------------------- K4: apply correction
-__global__ __launch_bounds__(256) void merge_apply_kernel(MergeArgs a) {
-  const int HW = a.g.H * a.g.W;
-  const size_t n = (size_t)a.n_out * 2 * HW;
-  const float mx = __uint_as_float(*a.absmax);
-  const bool too_high = __fdiv_rn(__fmul_rn(mx, 6.0f), a.smod) > 50.0f;   // KITTISampling.py:162
-  if (too_high) return;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int ol = i / (2 * HW);
-    const int rem = i % (2 * HW);
-    const int p = rem % HW;
-    const int o = a.o_begin + ol;
-    const size_t xi = (size_t)o * 2 * HW + rem;
-    if (!a.maskimg[(size_t)ol * HW + p] || a.refmask[xi] != 0) continue;
-    const float xv = a.xout[xi];
-    const float nv = a.newimg[((size_t)ol * 2) * HW + rem];
-    const float corr = -__fsub_rn(xv, nv);
-    a.xout[xi] = __fadd_rn(xv, __fmul_rn(a.cc, corr));
   }
 }
 
@@ -452,7 +472,8 @@ size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   add(npair * 4);                                            // pcell
   add(npair * 8);                                            // pcode
   add((size_t)n_out * 2 * H * W * 4);                        // newimg (internal)
-  add((size_t)n_out * H * W);                                // maskimg
+  add((size_t)n_src * H * W * 4);                            // isnap
+  add((T + 1) * 4);                                          // toff
   return b + 1024;
 }
 
@@ -484,29 +505,34 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   a.pcell = reinterpret_cast<int32_t*>(take(npair * 4));
   a.pcode = reinterpret_cast<double*>(take(npair * 8));
   a.newimg = new_out ? new_out : reinterpret_cast<float*>(take((size_t)a.n_out * 2 * H * W * 4));
-  a.maskimg = reinterpret_cast<uint8_t*>(take((size_t)a.n_out * H * W));
+  a.isnap = reinterpret_cast<float*>(take(nw * 4));
+  a.toff = reinterpret_cast<uint32_t*>(take(((size_t)T + 1) * 4));
   const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
   const size_t lds = (size_t)T * 4;
-  if (lds > 64 * 1024) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
-  // grids: sums / counts 0, nearest code and index all-ones (cnt..sumI and minkey..minidx are
-  // contiguous in the workspace)
+  if (lds + ((size_t)nb + 1) * 4 > 64 * 1024) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
   hipError_t e;
-  if ((e = hipMemsetAsync(a.cnt, 0, reinterpret_cast<char*>(a.minkey) - reinterpret_cast<char*>(a.cnt), st)) != hipSuccess)
-    return e;
-  if ((e = hipMemsetAsync(a.minkey, 0xFF, reinterpret_cast<char*>(a.tcount) - reinterpret_cast<char*>(a.minkey), st)) !=
-      hipSuccess)
-    return e;
-  hipLaunchKernelGGL(merge_world_kernel, dim3(grid_for(nw)), dim3(256), 0, st, a);
+  // seven dependent launches: world (+ grid reset, intensity snapshot) -> count -> block scan ->
+  // scatter (+ top scan, tile table) -> segment sums -> nearest index -> resolve + correction
+  hipLaunchKernelGGL(merge_world_kernel, dim3(grid_for(std::max(nw, (size_t)a.n_out * cells))), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_bin_count_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
   hipLaunchKernelGGL(merge_scan_block_kernel, dim3(nb), dim3(256), 0, st, a.tcount, nt, a.bsum);
-  hipLaunchKernelGGL(merge_scan_top_kernel, dim3(1), dim3(1024), 0, st, a.bsum, nb);
-  hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
+  hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), lds + ((size_t)nb + 1) * 4, st, a, per_chunk, nb);
   const int nseg = (int)((npair + MERGE_SEG - 1) / MERGE_SEG);   // upper bound: records <= pairs
-  hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), 0, st, a, nb);
-  hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), 0, st, a, nb);
-  hipLaunchKernelGGL(merge_resolve_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
+  const size_t tlds = ((size_t)T + 1) * 4;
+  static bool lds_attr = false;   // the tile table beside the segment passes' 57 KB of static LDS
+  if (!lds_attr) {
+    if ((e = hipFuncSetAttribute((const void*)merge_seg_sum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 96 * 1024)) != hipSuccess ||
+        (e = hipFuncSetAttribute((const void*)merge_seg_minidx_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 96 * 1024)) != hipSuccess)
+      return e;
+    lds_attr = true;
+  }
+  if (tlds > 96 * 1024) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
+  hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), tlds, st, a);
+  hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), tlds, st, a);
   if (apply_wait && (e = hipStreamWaitEvent(st, apply_wait, 0)) != hipSuccess) return e;   // tooHigh's global max
-  hipLaunchKernelGGL(merge_apply_kernel, dim3(grid_for(2 * nout)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(merge_resolve_apply_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 

@@ -17,39 +17,22 @@ static long floordiv(long a, long b) {  // Python // on ints
   return (r != 0 && ((r < 0) != (b < 0))) ? q - 1 : q;
 }
 
-// cos/sin of the azimuth / elevation of every column / row, float64 (KITTISampling.py:101-102)
-__global__ void merge_trig_kernel(double* trig, MergeGeom g, double vMin) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < g.W) {
-    const double az = (double)(g.W - 1 - i) * g.hA + g.hMin;
-    trig[i] = cos(az);
-    trig[g.W + i] = sin(az);
-  } else if (i < g.W + g.H) {
-    const int r = i - g.W;
-    const double el = (double)(g.H - 1 - r) * g.vA + vMin;
-    trig[2 * g.W + r] = cos(el);
-    trig[2 * g.W + g.H + r] = sin(el);
-  }
-}
-
 }  // namespace sdp
 
 using namespace sdp;
-
-static size_t trig_bytes(int H, int W) { return (((size_t)(2 * W + 2 * H) * 8 + 255) / 256) * 256; }
 
 extern "C" {
 
 int sdp_merge_workspace_size(int n_src, int n_out, int H, int W, size_t* bytes) {
   if (!bytes || n_src <= 0 || n_out <= 0 || H <= 0 || W <= 0) return sdp_fail("sdp_merge_workspace_size: bad argument");
-  *bytes = trig_bytes(H, W) + merge_ws_bytes(n_src, n_src, n_out, H, W);   // any megabatch size
+  *bytes = merge_ws_bytes(n_src, n_src, n_out, H, W);   // any megabatch size
   return 0;
 }
 
 int sdp_merge_workspace_bytes(int n_src, int aB, int n_out, int H, int W, size_t* bytes) {
   if (!bytes || n_src <= 0 || aB <= 0 || aB > n_src || n_out <= 0 || H <= 0 || W <= 0)
     return sdp_fail("sdp_merge_workspace_bytes: bad argument");
-  *bytes = trig_bytes(H, W) + merge_ws_bytes(n_src, aB, n_out, H, W);
+  *bytes = merge_ws_bytes(n_src, aB, n_out, H, W);
   return 0;
 }
 
@@ -62,8 +45,6 @@ int sdp_consistency_merge_ev(float* x_all, int n_src, int aB, int o_begin, int n
   if (prm->variant == SDP_MERGE_POSES && (!toWorld || !fromWorld))
     return sdp_fail("sdp_consistency_merge: POSES variant needs toWorld/fromWorld");
   if (prm->variant == SDP_MERGE_ORIGINS && !origins) return sdp_fail("sdp_consistency_merge: ORIGINS needs origins");
-  const size_t tb = trig_bytes(H, W);
-  if (ws_bytes < tb) return sdp_fail("sdp_consistency_merge: workspace too small");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   MergeArgs a{};
   MergeGeom& g = a.g;
@@ -75,7 +56,7 @@ int sdp_consistency_merge_ev(float* x_all, int n_src, int aB, int o_begin, int n
   g.hMin = (double)floordiv((long)W * -180, 360) * g.hA + g.hA / 2;
   g.big = (int)((50L * H) / 28);
   g.bigMin = (double)floordiv(g.big, -2) * g.vA + g.vA / 2;
-  const double vMin = (double)floordiv((long)H * -25, 28) * g.vA + g.vA / 2;
+  g.vMin = (double)floordiv((long)H * -25, 28) * g.vA + g.vA / 2;
   a.x = x_all;
   a.xout = x_all;
   a.toWorld = toWorld;
@@ -97,12 +78,8 @@ int sdp_consistency_merge_ev(float* x_all, int n_src, int aB, int o_begin, int n
   // log2(tensor(0.2)+1)/6*sigmaMod in float32 (KITTISampling.py:272-274)
   const float l2 = (float)std::log2((double)(0.2f + 1.0f));
   a.min_code = (l2 / 6.0f) * a.smod;
-  double* trig = reinterpret_cast<double*>(ws);
-  a.trig = trig;
-  hipLaunchKernelGGL(merge_trig_kernel, dim3((W + H + 255) / 256), dim3(256), 0, st, trig, g, vMin);
   const char* why = "merge";
-  hipError_t e = consistency_merge(a, reinterpret_cast<char*>(ws) + tb, ws_bytes - tb, new_images, st, &why,
-                                   reinterpret_cast<hipEvent_t>(absmax_event));
+  hipError_t e = consistency_merge(a, ws, ws_bytes, new_images, st, &why, reinterpret_cast<hipEvent_t>(absmax_event));
   if (e != hipSuccess) return sdp_fail(std::string("sdp_consistency_merge: ") + why + " " + hipGetErrorString(e));
   return 0;
 }
