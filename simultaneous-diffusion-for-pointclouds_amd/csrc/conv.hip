@@ -4,14 +4,26 @@
 
 namespace sdp {
 
+// The 16-wide 3x3 forward tiles on 32-Cout waves, two per SIMD (conv_launch_nj2): the 128-Cout layers
+// in both bf16 modes (4-wave workgroups, two per CU: 128->128 @64x1024 203.7 -> 184.4 us per fp32x3 B=4
+// launch in the network, line 333.7-336.1 -> 345.0-345.1 image-steps/s), the 256-Cout layers in bf16
+// (8-wave workgroups: 87.4 -> 80.8-85.4 us per B=4 launch; in fp32x3 they measured slower, 163.0 ->
+// 165.8 us, and keep one 64-Cout wave per SIMD) -- profiles/experiments/r05_nj2_ab.log.
+// SDP_CONV_NJ2=0 (build-time A/B only, tools/lib_variant.sh) restores the 64-Cout waves.
+#ifndef SDP_CONV_NJ2
+#define SDP_CONV_NJ2 1
+#endif
+
 template <int MODE, bool PELU>
 static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int tc, bool half, hipStream_t st) {
   if (ks == 1)   // the ConvMeanPool 1x1 shortcut: pooled epilogue (training), or on pre-pooled input (forward)
     return pool ? conv_launch<MODE, 1, 64, 1, true, PELU>(a, st) : conv_launch<MODE, 1, 64, 1, false, PELU>(a, st);
   if (pool) return conv_launch<MODE, 1, 64, 3, true, PELU>(a, st);
   if constexpr (MODE != MODE_F32) {   // 16-wide tiles: the 16x16 MFMA shape only
-    if (half) return conv_launch_half<MODE, PELU>(a, st);
-    if (tc == 16) return conv_launch<MODE, 1, 16, 3, false, PELU>(a, st);
+    if (half) return SDP_CONV_NJ2 ? conv_launch_nj2<MODE, PELU, 4>(a, st) : conv_launch_half<MODE, PELU>(a, st);
+    if (tc == 16)
+      return (SDP_CONV_NJ2 && MODE == MODE_BF16) ? conv_launch_nj2<MODE, PELU, 8>(a, st)
+                                                 : conv_launch<MODE, 1, 16, 3, false, PELU>(a, st);
   }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, PELU>(a, st);
   return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, PELU>(a, st) : conv_launch<MODE, 1, 32, 3, false, PELU>(a, st);
@@ -21,8 +33,9 @@ template <int MODE>
 static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int tc, hipStream_t st, bool half = false) {
 #ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
   if constexpr (MODE != MODE_F32) {
-    if (half) return conv_launch_half<MODE, true>(a, st);
-    return conv_launch<MODE, 1, 16, 3, false, true>(a, st);
+    if (half) return SDP_CONV_NJ2 ? conv_launch_nj2<MODE, true, 4>(a, st) : conv_launch_half<MODE, true>(a, st);
+    return (SDP_CONV_NJ2 && MODE == MODE_BF16) ? conv_launch_nj2<MODE, true, 8>(a, st)
+                                               : conv_launch<MODE, 1, 16, 3, false, true>(a, st);
   }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, true>(a, st);
   return conv_launch<MODE, 1, 32, 3, false, true>(a, st);

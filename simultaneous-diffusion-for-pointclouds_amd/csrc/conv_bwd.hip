@@ -15,6 +15,14 @@
 #endif
 
 
+// The 8 x 16 circular data gradients on 32-Cout waves, two per SIMD (dgrad_launch_nj2), as the forward:
+// the 128-Cout layers in both modes, the 256-Cout layers in bf16 (bf16 training step 151.2-151.8 ->
+// 151.7-152.5 image-steps/s, profiles/experiments/r05_dgrad_nj2_ab.log); SDP_DGRAD_NJ2=0 (build-time
+// A/B only) restores the 64-Cout waves
+#ifndef SDP_DGRAD_NJ2
+#define SDP_DGRAD_NJ2 1
+#endif
+
 namespace sdp {
 
 // 8 x 16 pixel tiles (the forward's: a 10 x 18 patch, 1.41x the pixels, against 4 x 66 = 2.06x for
@@ -33,7 +41,11 @@ static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, b
 #endif
   if (ks == 1) return dgrad_launch<MODE, 2, 32, 1, false>(a, st);
   if (!a.circular) return dgrad_launch<MODE, 2, 32, 3, true>(a, st);
-  if (t16) return wm == 2 ? dgrad_launch_half<MODE>(a, st) : dgrad_launch<MODE, 1, 16, 3, false>(a, st);
+  if (t16) {
+    if (wm == 2) return SDP_DGRAD_NJ2 ? dgrad_launch_nj2<MODE, 4>(a, st) : dgrad_launch_half<MODE>(a, st);
+    return (SDP_DGRAD_NJ2 && MODE == MODE_BF16) ? dgrad_launch_nj2<MODE, 8>(a, st)
+                                                : dgrad_launch<MODE, 1, 16, 3, false>(a, st);
+  }
   if (wm == 2) return dgrad_launch<MODE, 2, 32, 3, false>(a, st);
   return tc == 64 ? dgrad_launch<MODE, 1, 64, 3, false>(a, st) : dgrad_launch<MODE, 1, 32, 3, false>(a, st);
 }

@@ -2,8 +2,9 @@
 //
 // Built once per kernel shape (Makefile: conv_i_<code>.o with -DSDP_INST=<code>):
 //   forward : code = 100 * (mode + 1) + 10 * pelu + shape   (shape = index into FwdShape; 7 = the
-//             2-wave workgroups of conv_launch_half; 8 = the non-pooled 1x1)
-//   dgrad 2-wave workgroups: code = 1000 + 10 * mode + 6
+//             2-wave workgroups of conv_launch_half; 8 = the non-pooled 1x1; 9 / 6 = the 32-Cout waves
+//             of conv_launch_nj2 on 4 / 8 waves)
+//   dgrad 2-wave workgroups: code = 1000 + 10 * mode + 6; 32-Cout waves on 4 / 8 waves: + 7 / + 8
 //   dgrad   : code = 1000 + 10 * mode + shape                (shape = index into DgradShape)
 // Without SDP_INST (tools/conv_bench, -DSDP_CONV_BENCH_ONLY) it instantiates the 3x3 non-pooled
 // ELU-prologue forward shapes of every mode, which is all that bench dispatches.
@@ -17,6 +18,12 @@ namespace sdp {
 // power-limited load at the same cycles per FLOP (256->256 185 -> 171 us,
 // 128->128 @64x1024 227 -> 214 us).
 
+// SDP_FWD_TRN (diagnostic A/B builds only): the 16-wide forward tiles in the D = W x X orientation
+// with the transposed direct epilogue (16-B accesses), as the data gradient runs
+#ifndef SDP_FWD_TRN
+#define SDP_FWD_TRN 0
+#endif
+
 template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
 hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS>;
@@ -25,7 +32,8 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   a.strip_w = conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / TC);
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   if constexpr (MODE != MODE_F32) {
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16, 4, (SDP_FWD_TRN && TC == 16 && !POOL)>),
+                       grid, dim3(256), 0, st, a);
     return hipGetLastError();
   } else if constexpr (TC >= 32) {   // the 32x32 shape tiles rows in 32-pixel fragments
     hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU>), grid, dim3(256), 0, st, a);
@@ -42,7 +50,22 @@ hipError_t conv_launch_half(ConvArgs a, hipStream_t st) {
   a.strip_w = 0;   // row-major: strips cut this class's reads 229 -> 177 MB but cost 2.6 % of time
                    // (profiles/experiments/r03_strip_ab.log)
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, 2>), grid, dim3(T::NTH), 0, st, a);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, 2, (SDP_FWD_TRN != 0)>), grid,
+                     dim3(T::NTH), 0, st, a);
+  return hipGetLastError();
+}
+
+// 32-Cout waves, two per SIMD (conv_kernel.h ConvTile NJ = 2): 128 px x 128 Cout on 4 waves, two
+// workgroups per CU (pair), or 128 px x 256 Cout on 8 waves, one per CU (oct)
+template <int MODE, bool PELU, int NW>
+hipError_t conv_launch_nj2(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<1, 16, 3, NW, 2>;
+  a.tiles_per_img = a.H * a.W / (T::TR * 16);
+  a.groups_per_img = a.H * a.W / 128;
+  a.strip_w = NW == 8 ? conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / 16) : 0;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, NW, false, 2>), grid, dim3(T::NTH), 0,
+                     st, a);
   return hipGetLastError();
 }
 
@@ -79,6 +102,19 @@ hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st) {
   return hipGetLastError();
 }
 
+// data gradient on 32-Cout waves, two per SIMD (conv_kernel.h ConvTile NJ = 2, transposed epilogue):
+// 4 waves = 128 Cout per workgroup, two per CU; 8 waves = 256 Cout, one per CU
+template <int MODE, int NW>
+hipError_t dgrad_launch_nj2(ConvArgs a, hipStream_t st) {
+  using T = ConvTile<1, 16, 3, NW, 2>;
+  a.tiles_per_img = a.H * a.W / (T::TR * 16);
+  a.groups_per_img = a.H * a.W / 128;
+  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, false, 16, NW, true, 2>), grid, dim3(T::NTH), 0,
+                     st, a);
+  return hipGetLastError();
+}
+
 template <int S> struct DgradShape;
 template <> struct DgradShape<0> { static constexpr int WM = 2, TC = 32, KS = 1; static constexpr bool ZP = false; };
 template <> struct DgradShape<1> { static constexpr int WM = 2, TC = 32, KS = 3; static constexpr bool ZP = true; };
@@ -87,7 +123,11 @@ template <> struct DgradShape<3> { static constexpr int WM = 1, TC = 64, KS = 3;
 template <> struct DgradShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool ZP = false; };
 template <> struct DgradShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool ZP = false; };  // 16x16 shape only
 
-#if defined(SDP_INST) && SDP_INST < 1000 && SDP_INST % 10 == 7
+#if defined(SDP_INST) && SDP_INST < 1000 && (SDP_INST % 10 == 6 || SDP_INST % 10 == 9)
+constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10;
+static_assert(kMode >= 1 && kMode <= 2 && kPelu <= 1, "SDP_INST: bad 32-Cout-wave forward code");
+template hipError_t conv_launch_nj2<kMode, (kPelu != 0), SDP_INST % 10 == 9 ? 4 : 8>(ConvArgs, hipStream_t);
+#elif defined(SDP_INST) && SDP_INST < 1000 && SDP_INST % 10 == 7
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10;
 static_assert(kMode >= 1 && kMode <= 2 && kPelu <= 1, "SDP_INST: bad 2-wave forward code");
 template hipError_t conv_launch_half<kMode, (kPelu != 0)>(ConvArgs, hipStream_t);
@@ -98,6 +138,10 @@ static_assert(kMode >= 0 && kMode <= 2 && kPelu <= 1 && (kShape <= 5 || kShape =
               "SDP_INST: bad forward code");
 using FS = FwdShape<kShape>;
 template hipError_t conv_launch<kMode, FS::WM, FS::TC, FS::KS, FS::POOL, (kPelu != 0)>(ConvArgs, hipStream_t);
+#elif defined(SDP_INST) && (SDP_INST % 10 == 7 || SDP_INST % 10 == 8)
+constexpr int kMode = (SDP_INST / 10) % 10;
+static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16), "SDP_INST: bad dgrad code");
+template hipError_t dgrad_launch_nj2<kMode, SDP_INST % 10 == 7 ? 4 : 8>(ConvArgs, hipStream_t);
 #elif defined(SDP_INST) && SDP_INST % 10 == 6
 constexpr int kMode = (SDP_INST / 10) % 10;
 static_assert(SDP_INST / 100 == 10 && (kMode == MODE_F32X3 || kMode == MODE_BF16), "SDP_INST: bad dgrad code");
@@ -115,6 +159,10 @@ template hipError_t conv_launch<MODE_F32X3, 1, 16, 3, false, true>(ConvArgs, hip
 template hipError_t conv_launch<MODE_BF16, 1, 16, 3, false, true>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_half<MODE_F32X3, true>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_half<MODE_BF16, true>(ConvArgs, hipStream_t);
+template hipError_t conv_launch_nj2<MODE_F32X3, true, 4>(ConvArgs, hipStream_t);
+template hipError_t conv_launch_nj2<MODE_F32X3, true, 8>(ConvArgs, hipStream_t);
+template hipError_t conv_launch_nj2<MODE_BF16, true, 4>(ConvArgs, hipStream_t);
+template hipError_t conv_launch_nj2<MODE_BF16, true, 8>(ConvArgs, hipStream_t);
 #else
 #error "conv_inst.hip: build with -DSDP_INST=<code> (Makefile) or -DSDP_CONV_BENCH_ONLY (tools/conv_bench)"
 #endif

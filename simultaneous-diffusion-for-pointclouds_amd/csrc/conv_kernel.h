@@ -61,14 +61,18 @@ namespace sdp {
 constexpr int PSTRIDE = 144;  // bytes per staged patch pixel: 32 ch x (hi,lo bf16) or 32 x f32, + 16 pad
 
 // NW = waves per workgroup: 4 (one workgroup per CU), or 2 (128-pixel x 128-Cout workgroups, two
-// per CU: one's prologue and epilogue run under the other's MFMAs)
-template <int WM, int TC, int KS, int NW = 4>
+// per CU: one's prologue and epilogue run under the other's MFMAs).
+// NJ = 16-Cout fragments per wave: 4 (128 px x 64 Cout per wave, one wave per SIMD, 512 registers), or
+// 2 (128 px x 32 Cout, two waves per SIMD at 256 registers: one wave's prologue, epilogue and waits run
+// under its partner's MFMAs) -- NW = 4 with two workgroups per CU (128 Cout), or NW = 8 (256 Cout).
+template <int WM, int TC, int KS, int NW = 4, int NJ = 4>
 struct ConvTile {
   static constexpr int NTH = 64 * NW;              // threads per workgroup
   static constexpr int WN = NW / WM;               // waves along N
   static constexpr int RW = 128 / TC;              // pixel rows per wave
   static constexpr int TR = WM * RW;               // tile rows
-  static constexpr int NTILE = WN * 64;            // output channels per workgroup
+  static constexpr int NTILE = WN * 16 * NJ;       // output channels per workgroup
+  static constexpr int WPC = 4 * (NJ == 2 ? 2 : 1) / NW;   // workgroups per CU the kernel is sized for
   static constexpr int HALO = KS == 3 ? 1 : 0;
   static constexpr int PC = TC + 2 * HALO;
   static constexpr int PR = TR + 2 * HALO;
@@ -80,7 +84,7 @@ struct ConvTile {
   static constexpr int PIPE_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
   static constexpr int EPI_BYTES = WM * 64 * (NTILE + 8) * 4;   // LDS-staged epilogue (one half)
   static constexpr int LDS_BYTES = PIPE_BYTES > EPI_BYTES ? PIPE_BYTES : EPI_BYTES;
-  static_assert(LDS_BYTES * (4 / NW) <= 160 * 1024, "LDS budget (4 / NW workgroups per CU)");
+  static_assert(LDS_BYTES * WPC <= 160 * 1024, "LDS budget (WPC workgroups per CU)");
 };
 
 SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -92,7 +96,7 @@ SDP_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p);
 // issue cycles to other instructions, MI355X_MICROARCH.md constants).  Staging unit k (16 B of one
 // patch pixel) is transformed in tap tap_of(k): the units spread over all taps, and each unit's next
 // DMA follows its own transform, so it has a whole chunk to land.
-template <int NU, int NT>
+template <int NU, int NT, int NSTG_ = 5>
 struct XformPlan {
   static constexpr int tap_of(int k) { return k * NT / NU; }
   static constexpr int first(int tap) {
@@ -105,9 +109,16 @@ struct XformPlan {
     for (int k = 0; k < NU; ++k) n += tap_of(k) == tap ? 1 : 0;
     return n;
   }
-  static constexpr int NSTG = 5;   // transform stages of one piece (2 channels of a unit)
-  // block of stage slot q of Q in a tap: blocks 2 .. 31, evenly
-  static constexpr int stage_blk(int q, int Q) { return 2 + q * 30 / (Q > 0 ? Q : 1); }
+  static constexpr int max_count() {
+    int m = 0;
+    for (int t = 0; t < NT; ++t) m = count(t) > m ? count(t) : m;
+    return m;
+  }
+  // transform stages of one piece (2 channels of a unit): 5 in fp32x3 (both values per stage; its 3
+  // MFMAs per block leave 24 issue cycles), 8 in bf16 (one value per stage where it costs; 8 cycles)
+  static constexpr int NSTG = NSTG_;
+  // block of stage slot q of Q in a tap of NBLK blocks: blocks 2 .. NBLK-1, evenly
+  static constexpr int stage_blk(int q, int Q, int NBLK) { return 2 + q * (NBLK - 2) / (Q > 0 ? Q : 1); }
 };
 
 // SH: MFMA shape of the bf16 modes -- 32 = v_mfma_f32_32x32x16_bf16 (wave tile = 4 x 2 fragments
@@ -124,12 +135,14 @@ struct XformPlan {
 // D = W x X made the fp32x3 forward convs 2-3 % slower (256->256 165 -> 170 us, 128->128 @64x1024
 // 209 -> 213 us) while the bf16 training step ran 132.8 -> 137.0 image-steps/s with the transposed
 // direct epilogue on the data gradient (profiles/experiments/r03_trans_ab.log).
-template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4, bool TRN = false>
-__global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
+template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4, bool TRN = false,
+          int NJ = 4>
+__global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
   static_assert((SH == 32) == (MODE == MODE_F32), "bf16 modes: 16x16 shape; exact fp32: 32x32");
   static_assert(NW == 4 || (SH == 16 && !POOL), "2-wave workgroups: the 16x16 non-pooled forward only");
-  using T = ConvTile<WM, TC, KS, NW>;
+  static_assert(NJ == 4 || (SH == 16 && !POOL && KS == 3 && WM == 1), "32-Cout waves: the 16x16 3x3 tiles only");
+  using T = ConvTile<WM, TC, KS, NW, NJ>;
   constexpr int NTH = T::NTH;
   constexpr int NT = KS * KS;
   constexpr bool TRANS = TRN && SH == 16 && !POOL;
@@ -175,10 +188,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   const int Cin = a.Cin, Cout = a.Cout;
   const int nchunks = Cin / 32;
   const int NB = Cout / 32;
-  const int nbg0 = n0 / 32 + wn * 2;               // global 32-channel block of this wave's nb=0
+  const int f0 = n0 / 16 + wn * NJ;                // global 16-channel fragment of this wave's nj = 0
+  const int nbg0 = f0 / 2;                         // global 32-channel block of this wave's nb=0
 
   f32x16 acc[4][2];
-  f32x4 acc4[8][4];                                // SH == 16: [16-px group][16-Cout group]
+  f32x4 acc4[8][NJ];                               // SH == 16: [16-px group][16-Cout group]
   if constexpr (SH == 32) {
     static_for<0, 4>([&](auto i) {
       static_for<0, 2>([&](auto j) {
@@ -188,7 +202,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     });
   } else {
     static_for<0, 8>([&](auto i) {
-      static_for<0, 4>([&](auto j) {
+      static_for<0, NJ>([&](auto j) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc4[i][j][r] = 0.f;
       });
@@ -210,19 +224,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   // ring for the hi-only bf16 fragments measured 135.5 -> 134.4 image-steps/s in the bf16 training
   // step, profiles/experiments/r03_train_ring_wgrad_ab.log)
   constexpr int NBUF = (NT % 3 == 0) ? 3 : 2;
-  uint4 bq[NBUF][2][4];   // SH 32: [slot][nb][(s, hi/lo)]; SH 16: [slot][nj / 2][(nj % 2, hi/lo)]
+  uint4 bq[NBUF][NJ / 2][4];   // SH 32: [slot][nb][(s, hi/lo)]; SH 16: [slot][nj / 2][(nj % 2, hi/lo)]
   // SH 16: fragment nj (Couts 16 nj .. of the wave's 64) lane l needs Cout 16 nj + l % 16 and
   // channel group g = l / 16 (channels 8g .. 8g+7 of the chunk); the 32x32 packing stores Cout c,
   // channels 16 s + 8 h at lane c % 32 + 32 h, slot s -- so the lane reads from there
-  int wq16[4];
+  int wq16[NJ];
   const int wlo16 = __builtin_amdgcn_readfirstlane(c16 ? 1024 : 16);   // byte offset of the lo part
   {
     const int g = lane >> 4, h = g & 1, sg = g >> 1;
-    static_for<0, 4>([&](auto njc) {
+    static_for<0, NJ>([&](auto njc) {
       constexpr int nj = decltype(njc)::value;
       const int L = 16 * (nj & 1) + (lane & 15) + 32 * h;
       // "#frag16": [chunk][tap][16-Cout fragment][hi, lo][lane][16 B]
-      wq16[nj] = c16 ? ((nbg0 * 2 + nj) * 128 + lane) * 16 : ((nbg0 + (nj >> 1)) * 64 + L) * 64 + sg * 32;
+      wq16[nj] = c16 ? ((f0 + nj) * 128 + lane) * 16 : ((nbg0 + (nj >> 1)) * 64 + L) * 64 + sg * 32;
     });
   }
   auto load_b = [&](auto buf, int chunk, int tap) __attribute__((always_inline)) {
@@ -238,7 +252,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         bq[J][1][q] = make_uint4(v1.x, v1.y, v1.z, v1.w);
       });
     } else {
-      static_for<0, 4>([&](auto njc) {
+      static_for<0, NJ>([&](auto njc) {
         constexpr int nj = decltype(njc)::value;
         const u32x4 vh = __builtin_amdgcn_raw_buffer_load_b128(wrs, wq16[nj], so, 0);
         bq[J][nj >> 1][2 * (nj & 1)] = make_uint4(vh.x, vh.y, vh.z, vh.w);
@@ -501,12 +515,12 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         if constexpr (tap + 1 < NT)
           read_a(pat, std::integral_constant<int, tap + 1>{}, std::integral_constant<int, 0>{}, pre_hi, pre_lo);
         if constexpr (NT > 1) dmas();   // 1x1: after the blocks, behind this tap's raw reads
-        constexpr int NBLK = 32;
+        constexpr int NBLK = 8 * NJ;
         static_for<0, NBLK>([&](auto blk_c) {
           constexpr int blk = decltype(blk_c)::value;
           {
             // block = (half s of the px groups, Cout group nj, px group i of the half)
-            constexpr int s = blk >> 4, nj = (blk >> 2) & 3, i = blk & 3, mb = 4 * s + i;
+            constexpr int s = blk / (4 * NJ), nj = (blk / 4) % NJ, i = blk & 3, mb = 4 * s + i;
             const uint4 h4 = bq[CUR][nj >> 1][2 * (nj & 1)], l4 = bq[CUR][nj >> 1][2 * (nj & 1) + 1];
             const bf16x8 bhi = *reinterpret_cast<const bf16x8*>(&h4);
             const bf16x8 blo = *reinterpret_cast<const bf16x8*>(&l4);
@@ -554,8 +568,11 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
   //   blocks 0, 1            : the raw values of the units this tap transforms (XformPlan::tap_of)
   //   blocks 2 .. 31         : their transform, 5 stages per 2-channel piece
   //   blocks 30, 31          : the LDS-DMA of those units for the chunk after next (raw slot free)
-  using XP = XformPlan<NU, NT>;
-  constexpr int NQ = MODE == MODE_F32X3 ? 8 : 4;   // A reads per half tap = weight loads per tap
+  using XP = XformPlan<NU, NT, MODE == MODE_BF16 ? 8 : 5>;
+  constexpr int NQ = MODE == MODE_F32X3 ? 8 : 4;   // A reads per half tap
+  constexpr int NWL = NJ * (MODE == MODE_F32X3 ? 2 : 1);   // weight loads per tap
+  constexpr int NBLK = 8 * NJ;                     // MFMA blocks per tap: (half s, Cout fragment nj, px group i)
+  static_assert(NQ <= NBLK / 2 && 2 * NWL <= NBLK, "the tap's fillers fit its blocks");
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   // one A fragment: pixel group i of half s of tap `tap`, hi (LO = 0) or lo part
@@ -600,6 +617,37 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
         constexpr int pc = decltype(pc_c)::value, st = decltype(st_c)::value;
         constexpr int j = pc / 2, h = pc % 2, k = U0 + j, PB = 1 - P;
         if constexpr (SDP_KO & 2) return;
+        if constexpr (XP::NSTG == 8) {   // bf16: the same arithmetic one value at a time
+          const float4 v = xr[j];
+          const float4 sv = ssv[PB][h];
+          if constexpr (st == 0) {
+            py0[pc] = fmaf(h ? v.z : v.x, sv.x, sv.y);
+            if constexpr (PELU) pe0[pc] = fminf(py0[pc], 0.f);
+          } else if constexpr (st == 1) {
+            py1[pc] = fmaf(h ? v.w : v.y, sv.z, sv.w);
+            if constexpr (PELU) pe1[pc] = fminf(py1[pc], 0.f);
+          } else if constexpr (st == 2) {
+            if constexpr (PELU) pe0[pc] = __expf(pe0[pc]);
+          } else if constexpr (st == 3) {
+            if constexpr (PELU) pe1[pc] = __expf(pe1[pc]);
+          } else if constexpr (st == 4) {
+            if constexpr (PELU) py0[pc] = fmaxf(py0[pc], pe0[pc] - 1.0f);
+            if constexpr (ZP) py0[pc] = ((uvalid >> k) & 1u) ? py0[pc] : 0.f;
+          } else if constexpr (st == 5) {
+            if constexpr (PELU) py1[pc] = fmaxf(py1[pc], pe1[pc] - 1.0f);
+            if constexpr (ZP) py1[pc] = ((uvalid >> k) & 1u) ? py1[pc] : 0.f;
+          } else if constexpr (st == 6) {
+            typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+            bf16x2 hi;
+            hi[0] = (__bf16)py0[pc];
+            hi[1] = (__bf16)py1[pc];
+            phi[pc] = *reinterpret_cast<const uint32_t*>(&hi);
+          } else {
+            const int pix = (tid + k * NTH) >> 3;
+            *reinterpret_cast<uint32_t*>(lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 8 + h * 4) = phi[pc];
+          }
+          return;
+        }
         if constexpr (st == 0) {
           const float4 v = xr[j];
           const float4 sv = ssv[PB][h];
@@ -643,9 +691,9 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           if constexpr (MODE == MODE_F32X3) *reinterpret_cast<uint32_t*>(dst + 64) = plo[pc];
         }
       };
-      static_for<0, 32>([&](auto blk_c) {
+      static_for<0, NBLK>([&](auto blk_c) {
         constexpr int blk = decltype(blk_c)::value;
-        constexpr int s = blk >> 4, nj = (blk >> 2) & 3, i = blk & 3, mb = 4 * s + i;
+        constexpr int s = blk / (4 * NJ), nj = (blk / 4) % NJ, i = blk & 3, mb = 4 * s + i;
         // ---- fillers that feed this tap: raw reads first (the transform waits on them)
         if constexpr (blk < UN) xr[blk] = xform_load(std::integral_constant<int, U0 + blk>{});
         // ---- the block's MFMAs
@@ -671,24 +719,24 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
           }
         }
         // ---- fillers for later taps
-        if constexpr (blk < NQ) {   // this tap's half-1 fragments (used from block 16)
+        if constexpr (blk < NQ) {   // this tap's half-1 fragments (used from block NBLK / 2)
           constexpr int q = blk, ii = MODE == MODE_F32X3 ? (q >> 1) : q, lo = MODE == MODE_F32X3 ? (q & 1) : 0;
           cb[lo][ii] = read_a1(pat, tap_c, I1{}, std::integral_constant<int, ii>{}, std::integral_constant<int, lo>{});
         }
-        if constexpr ((blk & 1) && (blk >> 1) < NQ)   // tap + 2's weights
+        if constexpr ((blk & 1) && (blk >> 1) < NWL)   // tap + 2's weights
           load_b1(std::integral_constant<int, NXT>{}, std::integral_constant<int, (blk >> 1)>{}, wchunk, wtap);
-        if constexpr (tap + 1 < NT && blk >= 16 && blk < 16 + NQ) {   // tap + 1's half-0 fragments
-          constexpr int q = blk - 16, ii = MODE == MODE_F32X3 ? (q >> 1) : q, lo = MODE == MODE_F32X3 ? (q & 1) : 0;
+        if constexpr (tap + 1 < NT && blk >= NBLK / 2 && blk < NBLK / 2 + NQ) {   // tap + 1's half-0 fragments
+          constexpr int q = blk - NBLK / 2, ii = MODE == MODE_F32X3 ? (q >> 1) : q, lo = MODE == MODE_F32X3 ? (q & 1) : 0;
           ca[lo][ii] = read_a1(pat, std::integral_constant<int, tap + 1>{}, I0{}, std::integral_constant<int, ii>{},
                                std::integral_constant<int, lo>{});
         }
         static_for<0, Q>([&](auto q_c) {   // transform stages dealt to this block
           constexpr int q = decltype(q_c)::value;
-          if constexpr (XP::stage_blk(q, Q) == blk)
+          if constexpr (XP::stage_blk(q, Q, NBLK) == blk)
             stage(std::integral_constant<int, q / XP::NSTG>{}, std::integral_constant<int, q % XP::NSTG>{});
         });
-        if constexpr (UN > 0 && blk >= 32 - UN)   // the DMA of a transformed unit (its raw slot was read)
-          load_unit_o(std::integral_constant<int, U0 + blk - (32 - UN)>{}, chunk + 2);
+        if constexpr (UN > 0 && blk >= NBLK - UN)   // the DMA of a transformed unit (its raw slot was read)
+          load_unit_o(std::integral_constant<int, U0 + blk - (NBLK - UN)>{}, chunk + 2);
         __builtin_amdgcn_sched_barrier(0);
       });
     });
@@ -697,8 +745,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     if constexpr (!(SDP_KO & 8)) __builtin_amdgcn_s_barrier();
   };
   static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
-  if constexpr (MODE != MODE_F32 && NT == 9) {
-    static_assert(XP::count(0) <= 2 && XP::NSTG * 2 * 2 <= 30, "one filler slot per block");
+  // (the data-gradient launches keep do_chunk: in bf16 training the tap schedule measured 3-5 % slower
+  // on them, profiles/experiments/r05_train_kernel_stats_ab.log)
+  if constexpr (MODE != MODE_F32 && NT == 9 && !TRANS) {
+    static_assert(XP::max_count() * 2 * XP::NSTG <= 2 * (NBLK - 2), "at most two transform stages per block");
     for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
       do_chunk9(std::integral_constant<int, 0>{}, chunk);
       do_chunk9(std::integral_constant<int, 1>{}, chunk + 1);
@@ -733,7 +783,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     auto soff = [&](int mb, int nj) {                // wave-uniform part: fragment mb's first pixel, channel block nj
       const int mr = mb / CB, mc = (mb % CB) * 16;
       const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc) * d + ph_c;
-      return __builtin_amdgcn_readfirstlane(((y * Wo + x) * Cout + n0 + wn * 64 + nj * 16) * 4);
+      return __builtin_amdgcn_readfirstlane(((y * Wo + x) * Cout + n0 + wn * 16 * NJ + nj * 16) * 4);
     };
     auto ld = [&](__amdgpu_buffer_rsrc_t r, int so) {
       const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, voff, so, 0);
@@ -747,10 +797,10 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     auto rs_or_out = [&](const float* p) { return rs(p ? p : a.out); };
     const __amdgpu_buffer_rsrc_t ors = rs(a.out), xrs = rs_or_out(a.aux), rrs = rs_or_out(a.res), o2rs = rs_or_out(a.out2),
                                  r2rs = rs_or_out(a.res2);
-    static_for<0, 4>([&](auto njc) {
+    static_for<0, NJ>([&](auto njc) {
       constexpr int nj = decltype(njc)::value;
       __builtin_amdgcn_sched_barrier(0);              // one channel block at a time (register pressure)
-      const int co0 = n0 + wn * 64 + nj * 16 + 4 * lq;   // the lane's 4 channels
+      const int co0 = n0 + wn * 16 * NJ + nj * 16 + 4 * lq;   // the lane's 4 channels
       // every read of the block first -- the elu' operand, its (scale, shift), the residual -- so they
       // share one HBM round trip: issued where they are used, the residual's loads waited behind the
       // elu' math (data gradient 310 -> 260 us per 256->256 B=8 launch, bf16 training step 136.1 ->
@@ -896,7 +946,7 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     int vbase[NF];
     static_for<0, NF>([&](auto fc) {
       constexpr int f = decltype(fc)::value;
-      const int co = n0 + wn * 64 + lcol;
+      const int co = n0 + wn * 16 * NJ + lcol;
       if constexpr (POOL) {
         vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 16) >> 1) + 2 * lq) * Cout + co) * 4;
       } else {
@@ -910,19 +960,19 @@ __global__ __launch_bounds__(64 * NW, 1) void conv_mfma_kernel(ConvArgs a) {
     // are loaded before the first store: loads and stores retire through one in-order counter on gfx9,
     // so a block's loads issued after the previous block's stores would wait for their acknowledgement
     // too (line 328.2 -> 335.1 image-steps/s, profiles/experiments/r04_epilogue_preload_ab.log)
-    float pre[4][NV], biasv[4];
-    static_for<0, 4>([&](auto nj) { biasv[nj] = a.bias ? a.bias[n0 + wn * 64 + nj * 16 + lcol] : 0.f; });
+    float pre[NJ][NV], biasv[NJ];
+    static_for<0, NJ>([&](auto nj) { biasv[nj] = a.bias ? a.bias[n0 + wn * 16 * NJ + nj * 16 + lcol] : 0.f; });
     if (a.res || a.out2) {
       const __amdgpu_buffer_rsrc_t prs = a.res ? rrs : r2rs;
-      static_for<0, 4>([&](auto njc) {
+      static_for<0, NJ>([&](auto njc) {
 #pragma unroll
         for (int i = 0; i < NV; ++i)
           pre[njc][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, SDP_EPI16_OFF(i, decltype(njc)::value), 0));
       });
     }
-    static_for<0, 4>([&](auto njc) {
+    static_for<0, NJ>([&](auto njc) {
       constexpr int nj = decltype(njc)::value;
-      const int co = n0 + wn * 64 + nj * 16 + lcol;
+      const int co = n0 + wn * 16 * NJ + nj * 16 + lcol;
       const float bias = biasv[nj];
       float v[NV];
       if constexpr (POOL) {

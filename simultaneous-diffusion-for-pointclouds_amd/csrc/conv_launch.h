@@ -16,9 +16,18 @@ hipError_t conv_launch(ConvArgs a, hipStream_t st);
 template <int MODE, bool PELU>
 hipError_t conv_launch_half(ConvArgs a, hipStream_t st);
 
+// forward of the 16-wide 3x3 tiles on 32-Cout waves, two per SIMD (conv_inst.hip shapes 9 / 6): NW = 4
+// (128 Cout per workgroup, two per CU) or 8 (256 Cout, one per CU)
+template <int MODE, bool PELU, int NW>
+hipError_t conv_launch_nj2(ConvArgs a, hipStream_t st);
+
 // data gradient of the 128-channel layers on 2-wave workgroups (conv_inst.hip dgrad shape 6)
 template <int MODE>
 hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st);
+
+// data gradient of the 16-wide 3x3 tiles on 32-Cout waves, two per SIMD (conv_inst.hip dgrad shapes 7 / 8)
+template <int MODE, int NW>
+hipError_t dgrad_launch_nj2(ConvArgs a, hipStream_t st);
 
 // data gradient (conv_bwd.hip dispatch)
 template <int MODE, int WM, int TC, int KS, bool ZP>
