@@ -9,9 +9,16 @@ namespace sdp {
 // launch in the network, line 333.7-336.1 -> 345.0-345.1 image-steps/s), the 256-Cout layers in bf16
 // (8-wave workgroups: 87.4 -> 80.8-85.4 us per B=4 launch; in fp32x3 they measured slower, 163.0 ->
 // 165.8 us, and keep one 64-Cout wave per SIMD) -- profiles/experiments/r05_nj2_ab.log.
-// SDP_CONV_NJ2=0 (build-time A/B only, tools/lib_variant.sh) restores the 64-Cout waves.
+// The fp32x3 256-Cout layers run as two of those 128-Cout workgroups per tile (the patch is staged
+// twice, and 8 waves per CU hide each other's phases): line 348.6-348.9 -> 356.6-357.5
+// image-steps/s, 256->256 160.9-162.4 -> 159.7-161.5 us per launch (profiles/experiments/
+// r05_pair256_ab.log).  SDP_CONV_NJ2=0 (build-time A/B only, tools/lib_variant.sh) restores the
+// 64-Cout waves; SDP_CONV_NJ2_BF16_W8 picks the 8-wave workgroups for the bf16 256-Cout layers.
 #ifndef SDP_CONV_NJ2
 #define SDP_CONV_NJ2 1
+#endif
+#ifndef SDP_CONV_NJ2_BF16_W8
+#define SDP_CONV_NJ2_BF16_W8 1
 #endif
 
 template <int MODE, bool PELU>
@@ -21,9 +28,11 @@ static hipError_t launch_elu(const ConvArgs& a, int ks, bool pool, int wm, int t
   if (pool) return conv_launch<MODE, 1, 64, 3, true, PELU>(a, st);
   if constexpr (MODE != MODE_F32) {   // 16-wide tiles: the 16x16 MFMA shape only
     if (half) return SDP_CONV_NJ2 ? conv_launch_nj2<MODE, PELU, 4>(a, st) : conv_launch_half<MODE, PELU>(a, st);
-    if (tc == 16)
-      return (SDP_CONV_NJ2 && MODE == MODE_BF16) ? conv_launch_nj2<MODE, PELU, 8>(a, st)
-                                                 : conv_launch<MODE, 1, 16, 3, false, PELU>(a, st);
+    if (tc == 16) {   // the 256-Cout layers: two 128-Cout workgroups per tile (fp32x3), one 8-wave one (bf16)
+      if (!SDP_CONV_NJ2) return conv_launch<MODE, 1, 16, 3, false, PELU>(a, st);
+      return (MODE == MODE_BF16 && SDP_CONV_NJ2_BF16_W8) ? conv_launch_nj2<MODE, PELU, 8>(a, st)
+                                                         : conv_launch_nj2<MODE, PELU, 4>(a, st);
+    }
   }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, PELU>(a, st);
   return tc == 64 ? conv_launch<MODE, 1, 64, 3, false, PELU>(a, st) : conv_launch<MODE, 1, 32, 3, false, PELU>(a, st);
@@ -34,8 +43,9 @@ static hipError_t launch_mode(const ConvArgs& a, int ks, bool pool, int wm, int 
 #ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench: only the 3x3 non-pooled ELU-prologue kernels
   if constexpr (MODE != MODE_F32) {
     if (half) return SDP_CONV_NJ2 ? conv_launch_nj2<MODE, true, 4>(a, st) : conv_launch_half<MODE, true>(a, st);
-    return (SDP_CONV_NJ2 && MODE == MODE_BF16) ? conv_launch_nj2<MODE, true, 8>(a, st)
-                                               : conv_launch<MODE, 1, 16, 3, false, true>(a, st);
+    if (!SDP_CONV_NJ2) return conv_launch<MODE, 1, 16, 3, false, true>(a, st);
+    return (MODE == MODE_BF16 && SDP_CONV_NJ2_BF16_W8) ? conv_launch_nj2<MODE, true, 8>(a, st)
+                                                       : conv_launch_nj2<MODE, true, 4>(a, st);
   }
   if (wm == 2) return conv_launch<MODE, 2, 32, 3, false, true>(a, st);
   return conv_launch<MODE, 1, 32, 3, false, true>(a, st);

@@ -23,12 +23,13 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "simultaneous-diffusion-for-pointclouds_amd"))
 
-# label, kernel-name substring, threads per image-launch (grid per view), FLOP per view, MFMA passes, conv_bench C
+# label, kernel-name substring, threads per view along x (grid x), grid y (Cout / 128), FLOP per view,
+# MFMA passes, conv_bench C.  Both classes run conv_launch_nj2's 4-wave 128-Cout workgroups (NJ = 2):
+# the 256-Cout layers as two per tile (grid y = 2)
+NJ2 = "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false, 2>"
 CLASSES = [
-    ("conv3x3 256->256 @32x512 d1", "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false>", 128 * 256,
-     2 * 256 * 256 * 9 * 32 * 512, 3, 256),
-    ("conv3x3 128->128 @64x1024 d1", "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 2, false>", 512 * 128,
-     2 * 128 * 128 * 9 * 64 * 1024, 3, 128),
+    ("conv3x3 256->256 @32x512 d1", NJ2, 128 * 256, 2, 2 * 256 * 256 * 9 * 32 * 512, 3, 256),
+    ("conv3x3 128->128 @64x1024 d1", NJ2, 512 * 256, 1, 2 * 128 * 128 * 9 * 64 * 1024, 3, 128),
 ]
 
 
@@ -38,17 +39,19 @@ def load(d):
     for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             disp[r["Dispatch_Id"]] = {"name": r["Kernel_Name"], "grid": int(r["Grid_Size_X"]),
+                                      "gy": int(r.get("Grid_Size_Y", 1) or 1),
                                       "ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), "c": {}}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            e = disp.setdefault(r["Dispatch_Id"], {"name": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "ns": 0, "c": {}})
+            e = disp.setdefault(r["Dispatch_Id"], {"name": r["Kernel_Name"], "grid": int(r["Grid_Size"]), "gy": 1, "ns": 0,
+                                                   "c": {}})
             e["c"][r["Counter_Name"]] = e["c"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
     return disp
 
 
-def select(disp, sub, grid, skip=0):
+def select(disp, sub, grid, gy, skip=0):
     sel = [disp[k] for k in sorted(disp, key=int) if sub in disp[k]["name"] and disp[k]["grid"] == grid
-           and disp[k]["ns"] and disp[k]["c"]]
+           and disp[k]["gy"] == gy and disp[k]["ns"] and disp[k]["c"]]
     return sel[skip:]
 
 
@@ -63,11 +66,11 @@ def main():
            "how": __doc__.split("Writes")[0].strip()}
     # 1. GRBM vs in-kernel clock on isolated launches (conv_bench_T dispatches the library's kernel)
     cal = {}
-    for label, sub, gpv, flop, npass, C in CLASSES:
+    for label, sub, gpv, gy, flop, npass, C in CLASSES:
         for B in (4, 32):
             tag = f"cb_{C}_b{B}"
             ik = re.search(r"in-kernel clock ([0-9.]+) GHz", open(os.path.join(out, tag + ".ik.log")).read())
-            sel = select(load(os.path.join(out, tag)), "conv_mfma_kernel", gpv * B, skip=3)
+            sel = select(load(os.path.join(out, tag)), "conv_mfma_kernel", gpv * B, gy, skip=3)
             if not ik or not sel:
                 continue
             ns = avg(sel, lambda v: v["ns"])
@@ -81,11 +84,11 @@ def main():
                                        "mfma_busy_cycles_per_mfma": round(busy / n_mfma, 3),
                                        "mfma_busy_frac": round(busy / (float(ik.group(1)) * ns * 1024), 4)})
     # 2. the network
-    for label, sub, gpv, flop, npass, C in CLASSES:
+    for label, sub, gpv, gy, flop, npass, C in CLASSES:
         row = {"class": label}
         for V in (4, 16):
-            g = select(load(os.path.join(out, f"g_v{V}")), sub, gpv * V)
-            m = select(load(os.path.join(out, f"m_v{V}")), sub, gpv * V)
+            g = select(load(os.path.join(out, f"g_v{V}")), sub, gpv * V, gy)
+            m = select(load(os.path.join(out, f"m_v{V}")), sub, gpv * V, gy)
             if not g or not m:
                 continue
             ns = (avg(g, lambda v: v["ns"]) + avg(m, lambda v: v["ns"])) / 2
