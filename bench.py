@@ -295,7 +295,7 @@ def run_sampling(args, rank, N, dist, dev):
         else:
             merger(x_all, sig[c], setting, 10, 0.01, absmax, absmax_event=ev)
 
-    # consistency merge (9 kernels on the forward's stream), SURVEY §8(d) compulsory bytes per
+    # consistency merge (7 kernels on the forward's stream), SURVEY §8(d) compulsory bytes per
     # megabatch-step: per source view read x + mask + exist/sky, per output view write x and its
     # 114 x W accumulator grid written and read (24 B per cell) -- 7.3 MB per view at N = 1
     HWp = H * W
@@ -345,7 +345,7 @@ def run_sampling(args, rank, N, dist, dev):
                 mem.append({"kernel": k, "launches_per_step": round(n_ / steps, 2), "avg_launch_us": round(t_ * 1e6, 2),
                             "algorithmic_bytes": int(by_), "achieved_GBps": round(by_ / t_ / 1e9, 1),
                             "frac": round(by_ / t_ / 1e9 / HBM_PEAK, 4)})
-        mem.append({"kernel": "consistency_merge (9 kernels, HIP events around sdp_consistency_merge)",
+        mem.append({"kernel": "consistency_merge (7 kernels, HIP events around sdp_consistency_merge)",
                     "launches_per_step": 1, "avg_launch_us": round(merge_us, 2), "algorithmic_bytes": int(merge_bytes),
                     "achieved_GBps": round(merge_bytes / (merge_us * 1e-6) / 1e9, 1),
                     "frac": round(merge_bytes / (merge_us * 1e-6) / 1e9 / HBM_PEAK, 4),

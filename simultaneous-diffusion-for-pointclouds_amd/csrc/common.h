@@ -81,6 +81,9 @@ struct ConvArgs {
   int strip_w;             // tile order inside a phase sub-grid: 0 = row-major, else strips of strip_w tile
                            //   columns x all tile rows (set by the launcher, conv_strip_w)
   int groups_per_img;      // 128-pixel statistics groups per image (H*W/128)
+  int cpair;               // 1: grid.x deals (tile, Cout block) pairs, the block in bit 0 of the XCD-ordered index
+                           //   (both Cout halves of a tile on one XCD, back to back: the second patch read
+                           //   hits its L2); 0: Cout block = blockIdx.y (set by the launcher)
   unsigned long long* dbg; // diagnostics builds only (SDP_TIMING): per-workgroup phase clocks
   // backward epilogue (data gradient): out *= elu'(...) of `aux` (layout of out) before +res;
   // dact 0 = off, 1 = aux is the pre-activation, 2 = aux is the ELU output, 3 = aux is the

@@ -24,6 +24,12 @@ namespace sdp {
 #define SDP_FWD_TRN 0
 #endif
 
+// SDP_CONV_CPAIR=0 (build-time A/B only): the two Cout blocks of a tile on grid.y (dispatched a whole
+// grid row apart, the second patch read from HBM)
+#ifndef SDP_CONV_CPAIR
+#define SDP_CONV_CPAIR 1
+#endif
+
 template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
 hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS>;
@@ -63,7 +69,10 @@ hipError_t conv_launch_nj2(ConvArgs a, hipStream_t st) {
   a.tiles_per_img = a.H * a.W / (T::TR * 16);
   a.groups_per_img = a.H * a.W / 128;
   a.strip_w = NW == 8 ? conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / 16) : 0;
-  dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
+  // two Cout blocks per tile (the fp32x3 256-Cout layers on 4-wave workgroups): dealt as adjacent pairs
+  // of the XCD-ordered index, so a tile's second patch read comes from that XCD's L2
+  a.cpair = (SDP_CONV_CPAIR && a.Cout == 2 * T::NTILE) ? 1 : 0;
+  dim3 grid(a.B * a.tiles_per_img * (a.cpair ? 2 : 1), a.cpair ? 1 : a.Cout / T::NTILE);
   hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, NW, false, 2>), grid, dim3(T::NTH), 0,
                      st, a);
   return hipGetLastError();

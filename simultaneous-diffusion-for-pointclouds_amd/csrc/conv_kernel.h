@@ -165,6 +165,8 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   // contiguous range of tiles -- vertically adjacent tiles share their halo rows in its L2
   const int nwg = gridDim.x;
   int t = (nwg & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (nwg >> 3) + ((int)blockIdx.x >> 3);
+  const int cblk = a.cpair ? (t & 1) : (int)blockIdx.y;
+  if (a.cpair) t >>= 1;
   const int b = t / a.tiles_per_img;
   const int tile = t - b * a.tiles_per_img;
   t = tile;
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     tcol = t % tiles_c;
   }
   const int sr0 = trow * T::TR, sc0 = tcol * TC;
-  const int n0 = blockIdx.y * T::NTILE;
+  const int n0 = cblk * T::NTILE;
   const int wrow0 = wm * T::RW;                    // wave's first tile row
 
   const int Cin = a.Cin, Cout = a.Cout;

@@ -45,21 +45,28 @@ struct WgTile {
   static constexpr int NUD = 16;                        // dy tile: 128 px x 128 co / 4 / 256
   static constexpr int DY_PLANE = 4 * 128 * 64;         // [wave][px][32 co] bf16
   static constexpr int A_PLANE = NPIX * 64;             // [px][32 ci] bf16
+  static constexpr int RAW_DY = 64 * 128 * 4;           // OCC 3: one half of the fp32 dy tile, landed by LDS-DMA
 };
 
 // OCC: 1 = one workgroup per CU, next tile's loads in registers (fp32x3); 2 = two workgroups per CU
 // taking turns, chunked staging (bf16: 134.4 image-steps/s in the bf16 training step against 119.2
 // for OCC 1 and for one workgroup per CU with the next two tiles' loads in flight,
-// profiles/experiments/r03_train_ring_wgrad_ab.log)
+// profiles/experiments/r03_train_ring_wgrad_ab.log); 3 = two workgroups per CU, the dy tile landed by
+// LDS-DMA in two 32-KB halves (no registers), the next tile's first half issued before this tile's
+// MFMAs -- one exposed global round trip per tile (the second half, with the input patch's loads)
+// instead of four
 template <int MODE, int TC, int KS, int OCC>
-__global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
+__global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   using T = WgTile<TC, KS>;
   constexpr int NT = KS * KS;
   constexpr int NPL = MODE == MODE_F32X3 ? 2 : 1;      // bf16 planes: hi (+ lo)
-  __shared__ __attribute__((aligned(16))) char lds[NPL * (T::DY_PLANE + T::A_PLANE)];
+  constexpr int RAWB = OCC == 3 ? T::RAW_DY : 0;
+  static_assert(OCC != 3 || 2 * (NPL * (T::DY_PLANE + T::A_PLANE) + RAWB) <= 160 * 1024, "OCC 3: two workgroups per CU");
+  __shared__ __attribute__((aligned(16))) char lds[NPL * (T::DY_PLANE + T::A_PLANE) + RAWB];
   char* const dyL = lds;                                // plane pl at + pl * DY_PLANE
   char* const aL = lds + NPL * T::DY_PLANE;             // plane pl at + pl * A_PLANE
+  char* const rawL = lds + NPL * (T::DY_PLANE + T::A_PLANE);   // OCC 3
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
@@ -76,7 +83,7 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
   });
 
-  static_assert(OCC == 1 || OCC == 2, "OCC: 1 or 2");
+  static_assert(OCC >= 1 && OCC <= 3, "OCC: 1, 2 or 3");
   float4 rdS[1][T::NUD], raS[1][T::NUA];
   int tb = 0, tph_r = 0, tph_c = 0, tsr0 = 0, tsc0 = 0;
   auto decode = [&](int t) {
@@ -143,9 +150,13 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       return;
     }
     const float* inb = a.in + (size_t)tb * a.H * a.W * Cin + ci0;
+    // OCC 3: recompute the unit coordinates per tile (an opaque copy of tid): hoisted out of the tile
+    // loop they are ~30 loop-invariant VGPRs, spilled at two waves per SIMD
+    int tidv = tid;
+    if constexpr (OCC == 3) asm volatile("" : "+v"(tidv));
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
-      int u = tid + k * 256;
+      int u = tidv + k * 256;
       u = u < T::NPIX * 8 ? u : 0;
       const int pix = u >> 3, cv = u & 7;
       int sr = tsr0 - T::HALO + pix / T::PC, sc = tsc0 - T::HALO + pix % T::PC;
@@ -192,6 +203,8 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
     const float4* ra = raS[SET];
     const int sb = tb, sr0_ = tsr0, sc0_ = tsc0;
+    int tidv = tid;
+    if constexpr (OCC == 3) asm volatile("" : "+v"(tidv));
     const float* ssb = a.pro_ss + (size_t)sb * a.ss_bstride + ci0 * 2;
     // every unit of a thread has channel group cv = tid % 8: its (scale, shift) loaded once
     float4 s0 = make_float4(1.f, 0.f, 1.f, 0.f), s1 = s0;
@@ -201,7 +214,7 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     }
 #pragma unroll
     for (int k = KB; k < KE; ++k) {
-      const int u = tid + k * 256;
+      const int u = tidv + k * 256;
       if (u >= T::NPIX * 8) break;
       const int pix = u >> 3, cv = u & 7;
       float4 v = ra[k];
@@ -238,6 +251,45 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       load_a(KB{}, KE{}, I0{});
       store_a(KB{}, KE{}, I0{});
     });
+  };
+
+  // OCC 3: half h of the dy tile (tile pixels 64h .. 64h+63) lands in rawL by LDS-DMA.  Unit u =
+  // (wave * 8 + j) * 64 + lane, j < 8, is 16 B = 4 channels (u & 31) of tile pixel 64h + (u >> 5); it
+  // lands at rawL + 16u and is converted by the thread that issued it (its own vmcnt, no barrier)
+  // wave w's units are half pixels 16w + 2j + (lane >> 5): one tile row (TC >= 32), so unit j is unit
+  // 0 plus a wave-uniform 2j columns (SGPR offset) -- one VGPR offset per thread
+  static_assert(OCC != 3 || TC % 32 == 0, "OCC 3: a wave's 16 pixels inside one tile row");
+  int dyo = 0;
+  if constexpr (OCC == 3) {
+    const int p = (tid >> 6) * 16 + ((tid & 63) >> 5);
+    dyo = (((p / TC) * d * a.W + (p % TC) * d) * Cout + (tid & 31) * 4) * 4;
+  }
+  auto dma_dy_half = [&](int h) __attribute__((always_inline)) {
+    if constexpr (OCC == 3) {
+      const i32x4 rs = buffer_desc(a.dy + (size_t)tb * a.H * a.W * Cout, (uint32_t)img_dy_bytes);
+      const int hoff = ((((64 / TC) * h) * d) * a.W) * Cout * 4;   // 64 tile pixels = 64 / TC tile rows
+      const uint32_t l0 = (uint32_t)(uintptr_t)rawL + (uint32_t)(tid >> 6) * 8 * 1024;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dma16_lds_opaque(rs, l0 + j * 1024, dyo, dbase + hoff + j * 2 * d * Cout * 4);
+    }
+  };
+  // convert the thread's own 8 landed units of half h (fp32 -> bf16 [wave][px][32 co] rows, bias sums)
+  auto convert_dy_half = [&](int h) __attribute__((always_inline)) {
+    if constexpr (OCC == 3) {
+      const int lane_ = tid & 63, wv = tid >> 6;
+      // two batches of four (16 VGPRs of reads in flight beside the input patch's loads)
+      static_for<0, 2>([&](auto g) {
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int j = decltype(g)::value * 4 + jj;
+          const int u = (wv * 8 + j) * 64 + lane_, px = 64 * h + (u >> 5), cv = u & 31;
+          const float4 v = *reinterpret_cast<const float4*>(rawL + u * 16);
+          put_bf16(dyL, T::DY_PLANE, (cv >> 3) * (128 * 64) + px * 64 + (cv & 7) * 8, v);
+          bsum = make_float4(bsum.x + v.x, bsum.y + v.y, bsum.z + v.z, bsum.w + v.w);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
   };
 
   // transposed-read lane roles (ds_read_b64_tr_b16, 32x32x16 operand): lane l of 16-lane
@@ -282,7 +334,33 @@ __global__ __launch_bounds__(256, OCC == 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       });
     }
   };
-  {
+  if constexpr (OCC == 3) {
+    // raw holds the first half of tile t's dy (issued before the previous tile's MFMAs) at the loop top
+    if (t_begin < t_end) {
+      decode(t_begin);
+      prep_tile();
+      dma_dy_half(0);
+    }
+    for (int t = t_begin; t < t_end; ++t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's half-0 units have landed
+      convert_dy_half(0);
+      __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0): raw read before it is refilled
+      dma_dy_half(1);
+      load_a(I0{}, INA{}, I0{});                           // the input patch, beside the second half
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::NUA) : "memory");   // the half-1 DMA (older than the loads)
+      convert_dy_half(1);
+      store_a(I0{}, INA{}, I0{});
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __syncthreads();                                     // dyL / aL complete, raw free
+      if (t + 1 < t_end) {
+        decode(t + 1);
+        prep_tile();
+        dma_dy_half(0);                                    // lands under this tile's MFMAs
+      }
+      compute();
+      __syncthreads();                                     // dyL / aL read before the next tile rewrites them
+    }
+  } else {
     if (OCC == 1 && t_begin < t_end) {
       decode(t_begin);
       prep_tile();
@@ -384,15 +462,30 @@ size_t wgrad_part_floats(int S, int Cin, int Cout, int ks) { return (size_t)S * 
 template <int MODE, int OCC>
 static hipError_t wgrad_occ(const WgradArgs& a, int ks, int tc, dim3 grid, hipStream_t st) {
   if (ks == 1) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 1, OCC>), grid, dim3(256), 0, st, a);
-  else if (tc == 64) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3, OCC>), grid, dim3(256), 0, st, a);
+  else if (tc == 64 && OCC != 3) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3, OCC == 3 ? 2 : OCC>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3, OCC>), grid, dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
+// bf16: the dy tile by LDS-DMA (OCC 3) wherever its LDS fits twice per CU -- the 1x1 tiles and the
+// 4 x 32 tiles of the 3x3 convs (the 2 x 64 tiles' 66 x 4 patch does not: 161 KB); SDP_WGRAD_OCC3=0
+// (build-time A/B only) restores the chunked register staging
+#ifndef SDP_WGRAD_OCC3
+#define SDP_WGRAD_OCC3 1
+#endif
+
 template <int MODE>
 static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
   dim3 grid(S, a.Cin / 32, a.Cout / 128);
-  return wgrad_occ<MODE, MODE == MODE_BF16 ? 2 : 1>(a, ks, tc, grid, st);
+  if constexpr (MODE == MODE_BF16) {
+    if (SDP_WGRAD_OCC3) {
+      const int Ws = a.W / a.dil, Hs = a.H / a.dil;
+      if (ks == 1) return wgrad_occ<MODE, 3>(a, ks, tc, grid, st);
+      if (Ws % 32 == 0 && Hs % 4 == 0) return wgrad_occ<MODE, 3>(a, ks, 32, grid, st);
+    }
+    return wgrad_occ<MODE, 2>(a, ks, tc, grid, st);
+  }
+  return wgrad_occ<MODE, 1>(a, ks, tc, grid, st);
 }
 
 hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,

@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(REPO, "simultaneous-diffusion-for-pointclouds_am
 # the 256-Cout layers as two per tile (grid y = 2)
 NJ2 = "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false, 2>"
 CLASSES = [
-    ("conv3x3 256->256 @32x512 d1", NJ2, 128 * 256, 2, 2 * 256 * 256 * 9 * 32 * 512, 3, 256),
+    ("conv3x3 256->256 @32x512 d1", NJ2, 256 * 256, 1, 2 * 256 * 256 * 9 * 32 * 512, 3, 256),
     ("conv3x3 128->128 @64x1024 d1", NJ2, 512 * 256, 1, 2 * 128 * 128 * 9 * 64 * 1024, 3, 128),
 ]
 

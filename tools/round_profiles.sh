@@ -1,6 +1,6 @@
 #!/bin/bash
 # Every measurement committed under profiles/ for a round, in GPU sessions of <= 20 min:
-#   PART=1: smoke, GPU tests, PMC traffic of the dominant classes;  PART=2: the bench workloads;
+#   PART=1: smoke, GPU tests, PMC traffic and in-network clock of the dominant classes;  PART=2: the bench workloads;
 #   PART=3: rocprofv3 kernel stats (line + train); PART=all: the three in one call.  Stops at the first
 #   step that faults or times out.
 set -u
@@ -19,7 +19,8 @@ PART=${PART:-1}
 if [ "$PART" = 1 ] || [ "$PART" = all ]; then
 step smoke 300 python __graft_entry__.py smoke
 step pytest_gpu 850 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread
-step traffic 200 bash tools/class_traffic.sh
+step traffic 200 env ROUND=${ROUND:-r05} bash tools/class_traffic.sh
+step clock 500 env ROUND=${ROUND:-r05} bash tools/conv_clock.sh
 fi
 if [ "$PART" = 2 ] || [ "$PART" = all ]; then
 step bench 300 python bench.py --steps 20 --warmup 5
