@@ -21,6 +21,12 @@
 #include "common.h"
 #include "kernels.h"
 
+// SDP_WGRAD_KO (diagnostic builds only, wrong results): 1 = the B operand read once per k step (no per-tap
+// LDS reads), 2 = no staging (the MFMAs run on whatever the LDS holds)
+#ifndef SDP_WGRAD_KO
+#define SDP_WGRAD_KO 0
+#endif
+
 namespace sdp {
 
 typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 vbf16x4;
@@ -69,6 +75,14 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
   char* const rawL = lds + NPL * (T::DY_PLANE + T::A_PLANE);   // OCC 3
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // OCC 3: values derived from the thread index are recomputed where they are used (from an opaque copy
+  // of it): hoisted they are tens of loop-invariant VGPRs, spilled at two waves per SIMD, and a scratch
+  // reload before the MFMA loop would make it wait for the next tile's DMA (one vmcnt)
+  auto tidx = [&]() __attribute__((always_inline)) {
+    int t = tid;
+    if constexpr (OCC == 3) asm volatile("" : "+v"(t));
+    return t;
+  };
   const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
   const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c, tiles_img = tiles_rc * d * d;
   const int total = a.B * tiles_img;
@@ -138,13 +152,32 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       rd[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
     }
   };
+  // OCC 3: the prologue's (scale, shift) of the thread's channel group, loaded beside the patch (a load of
+  // their own after the patch's wait would be one more round trip per tile)
+  float4 ssa0 = make_float4(1.f, 0.f, 1.f, 0.f), ssa1 = ssa0;
   auto load_a = [&](auto kb_, auto ke_, auto set_) {
     constexpr int KB = decltype(kb_)::value, KE = decltype(ke_)::value, SET = decltype(set_)::value;
     float4* ra = raS[SET];
+    if constexpr (OCC == 3 && KB == 0) {
+      if (a.pro_mode != PRO_NONE) {
+        const float* ssb = a.pro_ss + (size_t)tb * a.ss_bstride + ci0 * 2 + (tidx() & 7) * 8;
+        ssa0 = *reinterpret_cast<const float4*>(ssb);
+        ssa1 = *reinterpret_cast<const float4*>(ssb + 4);
+      }
+    }
     if (interior) {
+      int tidv = tid;
+      if constexpr (OCC == 3) asm volatile("" : "+v"(tidv));
 #pragma unroll
       for (int k = KB; k < KE; ++k) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(irs, voff_a[k], ibase, 0);
+        int vo = voff_a[k];
+        if constexpr (OCC == 3) {   // recomputed per tile (7 loop-invariant VGPRs fewer)
+          int u = tidv + k * 256;
+          u = u < T::NPIX * 8 ? u : 0;
+          const int pix = u >> 3, cv = u & 7;
+          vo = (((pix / T::PC) * d * a.W + (pix % T::PC) * d) * Cin + cv * 4) * 4;
+        }
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(irs, vo, ibase, 0);
         ra[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
       }
       return;
@@ -168,7 +201,12 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
         sc = min(max(sc, 0), Ws - 1);
       }
       const int y = sr * d + tph_r, x = sc * d + tph_c;
-      ra[k] = *reinterpret_cast<const float4*>(inb + ((size_t)y * a.W + x) * Cin + cv * 4);
+      if constexpr (OCC == 3) {   // through the image's buffer resource: 32-bit offsets, no 64-bit addresses
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(irs, ((y * a.W + x) * Cin + ci0 + cv * 4) * 4, 0, 0);
+        ra[k] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+      } else {
+        ra[k] = *reinterpret_cast<const float4*>(inb + ((size_t)y * a.W + x) * Cin + cv * 4);
+      }
     }
   };
   auto put_bf16 = [&](char* base, int plane, int off, float4 v) {
@@ -208,7 +246,10 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
     const float* ssb = a.pro_ss + (size_t)sb * a.ss_bstride + ci0 * 2;
     // every unit of a thread has channel group cv = tid % 8: its (scale, shift) loaded once
     float4 s0 = make_float4(1.f, 0.f, 1.f, 0.f), s1 = s0;
-    if (a.pro_mode != PRO_NONE) {
+    if constexpr (OCC == 3) {
+      s0 = ssa0;
+      s1 = ssa1;
+    } else if (a.pro_mode != PRO_NONE) {
       s0 = *reinterpret_cast<const float4*>(ssb + (tid & 7) * 8);
       s1 = *reinterpret_cast<const float4*>(ssb + (tid & 7) * 8 + 4);
     }
@@ -259,34 +300,35 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
   // wave w's units are half pixels 16w + 2j + (lane >> 5): one tile row (TC >= 32), so unit j is unit
   // 0 plus a wave-uniform 2j columns (SGPR offset) -- one VGPR offset per thread
   static_assert(OCC != 3 || TC % 32 == 0, "OCC 3: a wave's 16 pixels inside one tile row");
-  int dyo = 0;
-  if constexpr (OCC == 3) {
-    const int p = (tid >> 6) * 16 + ((tid & 63) >> 5);
-    dyo = (((p / TC) * d * a.W + (p % TC) * d) * Cout + (tid & 31) * 4) * 4;
-  }
   auto dma_dy_half = [&](int h) __attribute__((always_inline)) {
     if constexpr (OCC == 3) {
+      const int tl = tidx();
+      const int p = (tl >> 6) * 16 + ((tl & 63) >> 5);
+      const int dyo = (((p / TC) * d * a.W + (p % TC) * d) * Cout + (tl & 31) * 4) * 4;
       const i32x4 rs = buffer_desc(a.dy + (size_t)tb * a.H * a.W * Cout, (uint32_t)img_dy_bytes);
       const int hoff = ((((64 / TC) * h) * d) * a.W) * Cout * 4;   // 64 tile pixels = 64 / TC tile rows
-      const uint32_t l0 = (uint32_t)(uintptr_t)rawL + (uint32_t)(tid >> 6) * 8 * 1024;
+      const uint32_t l0 = (uint32_t)(uintptr_t)rawL + (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6) * 8 * 1024;
 #pragma unroll
       for (int j = 0; j < 8; ++j) dma16_lds_opaque(rs, l0 + j * 1024, dyo, dbase + hoff + j * 2 * d * Cout * 4);
     }
   };
   // convert the thread's own 8 landed units of half h (fp32 -> bf16 [wave][px][32 co] rows, bias sums)
-  auto convert_dy_half = [&](int h) __attribute__((always_inline)) {
+  // unit j of the thread: raw + rb + 1024 j -> dyL + wb + 4096 h + 128 j (pixel 64h + 16 wave + 2j + lane / 32,
+  // channel quad lane % 32): two base VGPRs, the rest in the instructions' offset fields
+  auto convert_dy_half = [&](auto h_) __attribute__((always_inline)) {
     if constexpr (OCC == 3) {
-      const int lane_ = tid & 63, wv = tid >> 6;
+      constexpr int h = decltype(h_)::value;
+      const int tl = tidx();
+      const int rb = tl * 16 + (tl >> 6) * 7 * 1024;
+      const int wb = ((tl & 31) >> 3) * (128 * 64) + ((tl >> 6) * 16 + ((tl & 63) >> 5)) * 64 + (tl & 7) * 8;
       // two batches of four (16 VGPRs of reads in flight beside the input patch's loads)
       static_for<0, 2>([&](auto g) {
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int j = decltype(g)::value * 4 + jj;
-          const int u = (wv * 8 + j) * 64 + lane_, px = 64 * h + (u >> 5), cv = u & 31;
-          const float4 v = *reinterpret_cast<const float4*>(rawL + u * 16);
-          put_bf16(dyL, T::DY_PLANE, (cv >> 3) * (128 * 64) + px * 64 + (cv & 7) * 8, v);
+        static_for<0, 4>([&](auto jj) {
+          constexpr int j = decltype(g)::value * 4 + decltype(jj)::value;
+          const float4 v = *reinterpret_cast<const float4*>(rawL + rb + j * 1024);
+          put_bf16(dyL + wb, T::DY_PLANE, h * 4096 + j * 128, v);
           bsum = make_float4(bsum.x + v.x, bsum.y + v.y, bsum.z + v.z, bsum.w + v.w);
-        }
+        });
         __builtin_amdgcn_sched_barrier(0);
       });
     }
@@ -294,14 +336,14 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
 
   // transposed-read lane roles (ds_read_b64_tr_b16, 32x32x16 operand): lane l of 16-lane
   // group G supplies row q = (l & 15) >> 2 (K), columns 4p .. 4p+3, p = l & 3 (M or N)
-  const int G = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-  const int kq = 8 * (G >> 1) + q;                      // K of this lane's address, read r adds 4r
-  const int mcol = 16 * (G & 1) + 4 * p;                 // channel of this lane's address
-  const char* dy_rd = dyL + wave * (128 * 64) + mcol * 2;
-  const char* a_rd = aL + mcol * 2;
-
   // the MFMAs of the staged tile: 8 k steps of 16 pixels x all taps
   auto compute = [&]() __attribute__((always_inline)) {
+    const int tl = tidx(), ln = tl & 63;
+    const int G = ln >> 4, q = (ln & 15) >> 2, p = ln & 3;
+    const int kq = 8 * (G >> 1) + q;                      // K of this lane's address, read r adds 4r
+    const int mcol = 16 * (G & 1) + 4 * p;                 // channel of this lane's address
+    const char* dy_rd = dyL + __builtin_amdgcn_readfirstlane(tl >> 6) * (128 * 64) + mcol * 2;
+    const char* a_rd = aL + mcol * 2;
 #pragma unroll 1
     for (int s = 0; s < 8; ++s) {   // 16 pixels per k step
       const int k0 = 16 * s + kq, k1 = k0 + 4;
@@ -321,7 +363,7 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
         const bf16x8 bhi = bhi_n;
         bf16x8 blo;
         if constexpr (MODE == MODE_F32X3) blo = blo_n;
-        if constexpr (tap + 1 < NT) {
+        if constexpr (tap + 1 < NT && !(SDP_WGRAD_KO & 1)) {
           constexpr int toff = (KS == 3 ? ((tap + 1) / 3) * T::PC + (tap + 1) % 3 : 0) * 64;
           bhi_n = rd_b(toff, 0);
           if constexpr (MODE == MODE_F32X3) blo_n = rd_b(toff, T::A_PLANE);
@@ -342,15 +384,23 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       dma_dy_half(0);
     }
     for (int t = t_begin; t < t_end; ++t) {
+      if constexpr (SDP_WGRAD_KO & 2) {
+        __syncthreads();
+        compute();
+        continue;
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this thread's half-0 units have landed
-      convert_dy_half(0);
+      convert_dy_half(I0{});
       __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0): raw read before it is refilled
       dma_dy_half(1);
       load_a(I0{}, INA{}, I0{});                           // the input patch, beside the second half
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::NUA) : "memory");   // the half-1 DMA (older than the loads)
-      convert_dy_half(1);
+      convert_dy_half(std::integral_constant<int, 1>{});
       store_a(I0{}, INA{}, I0{});
-      __builtin_amdgcn_s_waitcnt(0xc07f);
+      // vmcnt(0) + lgkmcnt(0) as a real s_waitcnt: the compiler then counts nothing in flight (a patch unit
+      // past the patch has no use, so its load would stay pending and the MFMA loop's first register
+      // reuse would wait on it -- behind the next tile's DMA)
+      __builtin_amdgcn_s_waitcnt(0x0070);
       __syncthreads();                                     // dyL / aL complete, raw free
       if (t + 1 < t_end) {
         decode(t + 1);
