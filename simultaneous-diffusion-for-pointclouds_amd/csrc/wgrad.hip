@@ -13,7 +13,8 @@
 // row offset, and the 9 taps reuse one staged input patch.
 //
 // Workgroup (4 waves, one per SIMD): 128 Cout x 32 Cin x all taps; wave w owns Cout
-// [32w, 32w+32) -> 9 accumulators of 32x32.  Grid (split, Cin/32, Cout/128): the pixels are
+// [32w, 32w+32) -> 9 accumulators of 32x32.  Grid split x Cin/32 x Cout/128 (1-D, the channel blocks
+// of a split together on one XCD, see the kernel): the pixels are
 // split S ways, every workgroup walks its range of TR x TC pixel tiles (polyphase sub-grid
 // for dilated convs, like the forward) with the next tile's global loads in registers, and
 // writes its partial sums to part[split][tap][Cout][Cin]; conv_wgrad_reduce sums the splits
@@ -22,7 +23,8 @@
 #include "kernels.h"
 
 // SDP_WGRAD_KO (diagnostic builds only, wrong results): 1 = the B operand read once per k step (no per-tap
-// LDS reads), 2 = no staging (the MFMAs run on whatever the LDS holds)
+// LDS reads), 2 = no staging (the MFMAs run on whatever the LDS holds), 4 = OCC 3 without the input patch's
+// loads, 8 = OCC 3 without the dy DMAs
 #ifndef SDP_WGRAD_KO
 #define SDP_WGRAD_KO 0
 #endif
@@ -86,9 +88,17 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
   const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
   const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c, tiles_img = tiles_rc * d * d;
   const int total = a.B * tiles_img;
-  const int split = blockIdx.x, S = gridDim.x;
+  // 1-D grid of (pixel split, Cin block, Cout block), the channel blocks fastest, dealt to the XCDs in
+  // contiguous ranges: the Cin/32 workgroups that read the same dy tile (and the Cout/128 that read the
+  // same input patch) run together on one XCD and share it through its L2 (PMC reads 514 -> 378 MB per
+  // launch against the splits-fastest order; time unchanged, profiles/experiments/r05_wgrad_occ_ab.log)
+  const int ncb = (a.Cin / 32) * (a.Cout / 128), G = gridDim.x;
+  const int q = (G & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3);
+  const int S = G / ncb;
+  const int cb = q % ncb, cib = cb % (a.Cin / 32), cob = cb / (a.Cin / 32);
+  const int split = q / ncb;
   const int t_begin = (int)((long long)total * split / S), t_end = (int)((long long)total * (split + 1) / S);
-  const int ci0 = blockIdx.y * 32, co0 = blockIdx.z * 128;
+  const int ci0 = cib * 32, co0 = cob * 128;
   const int Cin = a.Cin, Cout = a.Cout;
 
   f32x16 acc[NT];
@@ -308,8 +318,9 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       const i32x4 rs = buffer_desc(a.dy + (size_t)tb * a.H * a.W * Cout, (uint32_t)img_dy_bytes);
       const int hoff = ((((64 / TC) * h) * d) * a.W) * Cout * 4;   // 64 tile pixels = 64 / TC tile rows
       const uint32_t l0 = (uint32_t)(uintptr_t)rawL + (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6) * 8 * 1024;
+      if constexpr (!(SDP_WGRAD_KO & 8))
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dma16_lds_opaque(rs, l0 + j * 1024, dyo, dbase + hoff + j * 2 * d * Cout * 4);
+        for (int j = 0; j < 8; ++j) dma16_lds_opaque(rs, l0 + j * 1024, dyo, dbase + hoff + j * 2 * d * Cout * 4);
     }
   };
   // convert the thread's own 8 landed units of half h (fp32 -> bf16 [wave][px][32 co] rows, bias sums)
@@ -393,7 +404,7 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
       convert_dy_half(I0{});
       __builtin_amdgcn_s_waitcnt(0xc07f);                  // lgkmcnt(0): raw read before it is refilled
       dma_dy_half(1);
-      load_a(I0{}, INA{}, I0{});                           // the input patch, beside the second half
+      if constexpr (!(SDP_WGRAD_KO & 4)) load_a(I0{}, INA{}, I0{});   // the input patch, beside the second half
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(T::NUA) : "memory");   // the half-1 DMA (older than the loads)
       convert_dy_half(std::integral_constant<int, 1>{});
       store_a(I0{}, INA{}, I0{});
@@ -440,7 +451,7 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
   }
   // bias partials (the ci-block-0 workgroups): bpart[split][Cout]; every thread's channel
   // group is tid & 31, its pixels tid >> 5 -> combine the 8 threads of a group through LDS
-  if (a.bpart && blockIdx.y == 0) {
+  if (a.bpart && cib == 0) {
     __syncthreads();
     float4* red = reinterpret_cast<float4*>(lds);
     red[tid] = bsum;
@@ -519,14 +530,17 @@ static hipError_t wgrad_occ(const WgradArgs& a, int ks, int tc, dim3 grid, hipSt
 
 // bf16: the dy tile by LDS-DMA (OCC 3) wherever its LDS fits twice per CU -- the 1x1 tiles and the
 // 4 x 32 tiles of the 3x3 convs (the 2 x 64 tiles' 66 x 4 patch does not: 161 KB); SDP_WGRAD_OCC3=0
-// (build-time A/B only) restores the chunked register staging
+// (build-time A/B only) restores the chunked register staging (bf16 training step 151.0-151.4 against
+// 152.0-152.5 image-steps/s with OCC 3, profiles/experiments/r05_wgrad_occ_ab.log, which also holds the
+// rejected stagings: the whole next tile by LDS-DMA on one workgroup per CU, 303 against 195 us per
+// launch, and part of the input patch prefetched in registers under the MFMAs, 214 against 200 us)
 #ifndef SDP_WGRAD_OCC3
 #define SDP_WGRAD_OCC3 1
 #endif
 
 template <int MODE>
 static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
-  dim3 grid(S, a.Cin / 32, a.Cout / 128);
+  dim3 grid(S * (a.Cin / 32) * (a.Cout / 128));
   if constexpr (MODE == MODE_BF16) {
     if (SDP_WGRAD_OCC3) {
       const int Ws = a.W / a.dil, Hs = a.H / a.dil;
