@@ -22,6 +22,12 @@
 #ifndef SDP_DGRAD_NJ2
 #define SDP_DGRAD_NJ2 1
 #endif
+// the bf16 256-Cout data gradients on one 8-wave workgroup per tile: training 159.3-159.8 against
+// 157.8-158.5 image-steps/s for two 4-wave 128-Cout ones (SDP_DGRAD_NJ2_BF16_W8=0, build-time A/B only;
+// profiles/experiments/r05_dgrad_w8_vs_w4_ab.log)
+#ifndef SDP_DGRAD_NJ2_BF16_W8
+#define SDP_DGRAD_NJ2_BF16_W8 1
+#endif
 
 namespace sdp {
 
@@ -43,8 +49,9 @@ static hipError_t launch_dgrad_mode(const ConvArgs& a, int ks, int wm, int tc, b
   if (!a.circular) return dgrad_launch<MODE, 2, 32, 3, true>(a, st);
   if (t16) {
     if (wm == 2) return SDP_DGRAD_NJ2 ? dgrad_launch_nj2<MODE, 4>(a, st) : dgrad_launch_half<MODE>(a, st);
-    return (SDP_DGRAD_NJ2 && MODE == MODE_BF16) ? dgrad_launch_nj2<MODE, 8>(a, st)
-                                                : dgrad_launch<MODE, 1, 16, 3, false>(a, st);
+    if (SDP_DGRAD_NJ2 && MODE == MODE_BF16)
+      return SDP_DGRAD_NJ2_BF16_W8 ? dgrad_launch_nj2<MODE, 8>(a, st) : dgrad_launch_nj2<MODE, 4>(a, st);
+    return dgrad_launch<MODE, 1, 16, 3, false>(a, st);
   }
   if (wm == 2) return dgrad_launch<MODE, 2, 32, 3, false>(a, st);
   return tc == 64 ? dgrad_launch<MODE, 1, 64, 3, false>(a, st) : dgrad_launch<MODE, 1, 32, 3, false>(a, st);
