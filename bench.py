@@ -220,6 +220,54 @@ def timed(step, args, dist, dev):
     return dt
 
 
+def viewsplit_layout(args, rank, N):
+    """(n_src, aB, o_begin): the megabatch views a rank's merge reads, its megabatch size and the first
+    of the V views the rank owns.  viewsplit: one megabatch of V*N views, rank r owns [r*V, (r+1)*V)
+    (its Philox counters start at o_begin * per_view4, sdp/sampling.py); megabatch: an independent
+    megabatch of V views per rank."""
+    V = args.views
+    if args.mode == "viewsplit":
+        n_src = V * N if args.megabatch_views is None else args.megabatch_views
+        if args.megabatch_views is not None and (N != 1 or n_src < V):
+            raise SystemExit("--megabatch-views emulates a larger megabatch on one GPU only")
+        return n_src, n_src, rank * V
+    return V, V, 0
+
+
+def dry_run_viewsplit(args, rank, N, dist):
+    """CPU/gloo rehearsal of the viewsplit step's bookkeeping (no GPU, no libsdp): the rank layout of
+    viewsplit_layout, the Philox counter offsets, the per-step all-gather of the megabatch and the
+    all_reduce(MAX) of tooHigh, with a deterministic stand-in for the update (a function of each view's
+    global index and its counter offset) and for the merge (every owned view pulled towards the
+    megabatch mean, corrected by the global max).  Returns the sha256 of the final megabatch images:
+    equal for every N when the exchange and the offsets are right (tests/test_bench_launcher_cpu.py)."""
+    import hashlib
+    V, H, W = args.views, 4, 32
+    n_all = V * N
+    n_src, aB, o_begin = viewsplit_layout(args, rank, N)
+    assert n_src == n_all
+    per_view4 = 2 * H * W // 4
+    g = torch.Generator().manual_seed(1234)
+    x_all = torch.rand(n_all, 2, H, W, generator=g, dtype=torch.float32)
+    x = x_all[o_begin:o_begin + V]
+    offset = o_begin * per_view4
+    for i in range(args.steps):
+        views = torch.arange(o_begin, o_begin + V, dtype=torch.float32).view(V, 1, 1, 1)
+        ctr = (offset + (views - o_begin) * per_view4) % 9973.0   # each view's own Philox counter
+        x.add_(torch.sin(x * 3.0 + ctr * 1e-3 + views) * np.float32(1e-2))
+        offset += n_src * per_view4
+        amax = x[:, 0].abs().max().reshape(1)
+        if dist:
+            parts = list(x_all.chunk(N))
+            torch.distributed.all_gather(parts, x.clone())
+            torch.distributed.all_reduce(amax, op=torch.distributed.ReduceOp.MAX)
+        mean = x_all.mean(0, keepdim=True)
+        x.add_((mean - x) * np.float32(0.05) / amax)
+    if dist:
+        torch.distributed.all_gather(list(x_all.chunk(N)), x.clone())
+    return hashlib.sha256(x_all.numpy().tobytes()).hexdigest()
+
+
 def run_sampling(args, rank, N, dist, dev):
     from sdp import _lib
     from sdp.merge import AbsmaxAllReduce, Merger, allforone_origins
@@ -228,15 +276,8 @@ def run_sampling(args, rank, N, dist, dev):
     from sdp.weights import get_sigmas_np
 
     H, W, V = 64, 1024, args.views
-    if args.mode == "viewsplit":
-        n_src = V * N if args.megabatch_views is None else args.megabatch_views
-        if args.megabatch_views is not None and (N != 1 or n_src < V):
-            raise SystemExit("--megabatch-views emulates a larger megabatch on one GPU only")
-        aB, o_begin = n_src, rank * V
-        sc = scene_views(n_src, H, W)
-    else:
-        n_src, aB, o_begin = V, V, 0
-        sc = scene_views(V, H, W, seed=1234 + rank)
+    n_src, aB, o_begin = viewsplit_layout(args, rank, N)
+    sc = scene_views(n_src, H, W) if args.mode == "viewsplit" else scene_views(V, H, W, seed=1234 + rank)
     net = ScoreNet(H=H, W=W, precision=args.precision).load_synthetic()
     g = torch.Generator(device=dev).manual_seed(1234)
     x_all = torch.rand(n_src, 2, H, W, device=dev, generator=g)
@@ -633,12 +674,14 @@ def main():
             torch.distributed.init_process_group("gloo")
             t = torch.tensor([rank], dtype=torch.int64)
             torch.distributed.all_reduce(t)
+            digest = dry_run_viewsplit(args, rank, world, dist)
             if rank == 0:
                 print(json.dumps({"dry_run": True, "n_gpus": world, "world_size": torch.distributed.get_world_size(),
-                                  "rank_sum": int(t.item())}))
+                                  "rank_sum": int(t.item()), "viewsplit_sha256": digest}))
             torch.distributed.destroy_process_group()
         else:
-            print(json.dumps({"dry_run": True, "n_gpus": 1, "world_size": 1, "rank_sum": 0}))
+            print(json.dumps({"dry_run": True, "n_gpus": 1, "world_size": 1, "rank_sum": 0,
+                              "viewsplit_sha256": dry_run_viewsplit(args, 0, 1, False)}))
         return
     from sdp import _build
     _build.ensure_built()          # a fresh checkout has no libsdp.so (git-ignored): build before any GPU call

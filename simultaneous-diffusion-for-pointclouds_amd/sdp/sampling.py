@@ -15,7 +15,8 @@ noise (parity tests); otherwise noise is Philox N(0,1) from ``seed``, one counte
 elements of the whole job, so ``noise_views=(first_view, total_views)`` lets a call that
 holds a contiguous slice of a larger job (megabatch sharding) draw that slice's noise.  ``dist_group`` makes
 tooHigh global across ranks (one 4-byte all_reduce(MAX) per merged step); with
-``view_shard=(rank, world)`` the call's views are one megabatch split across ranks: each
+``view_shard=(rank, world)`` the call's views are one megabatch split across ranks in
+contiguous blocks (``view_blocks``: the first megabatch % world ranks hold one view more): each
 rank passes only its own views, the megabatch images are all-gathered every merged step
 (the cross-view consistency gather) and each rank merges into its own views.
 Documented deviations: B=1 works for the kitti sampler (the reference's ``torch.squeeze``
@@ -174,13 +175,28 @@ def anneal_Langevin_dynamics_inpainting(x_mod, refer_image, refer_mask, scorenet
 
 
 def _gather_views(S, group):
-    """All-gather this rank's views into the megabatch buffer (RCCL over xGMI on GPUs)."""
+    """All-gather every rank's views into the megabatch buffer (RCCL over xGMI on GPUs).  Equal
+    blocks land in place; uneven ones (megabatch % world != 0) travel padded to the largest block
+    and are copied into place."""
     dist = torch.distributed
+    blocks = S.blocks
+    cmax = max(c for _, c in blocks)
+    if all(c == cmax for _, c in blocks):
+        if S.x_all.is_cuda:
+            dist.all_gather_into_tensor(S.x_all, S.x, group=group)
+        else:  # gloo: list form
+            parts = list(S.x_all.chunk(len(blocks)))
+            dist.all_gather(parts, S.x.clone(), group=group)
+        return
+    pad = torch.zeros((cmax,) + tuple(S.x.shape[1:]), dtype=S.x.dtype, device=S.dev)
+    pad[:S.B].copy_(S.x)
+    buf = torch.empty((len(blocks) * cmax,) + tuple(S.x.shape[1:]), dtype=S.x.dtype, device=S.dev)
     if S.x_all.is_cuda:
-        dist.all_gather_into_tensor(S.x_all, S.x, group=group)
-    else:  # gloo: list form
-        parts = list(S.x_all.chunk(S.x_all.shape[0] // S.B))
-        dist.all_gather(parts, S.x.clone(), group=group)
+        dist.all_gather_into_tensor(buf, pad, group=group)
+    else:
+        dist.all_gather(list(buf.chunk(len(blocks))), pad, group=group)
+    for r, (v0, c) in enumerate(blocks):
+        S.x_all[v0:v0 + c].copy_(buf[r * cmax:r * cmax + c])
 
 
 def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr, denoise, verbose, grad_ref, cc0,
@@ -223,15 +239,29 @@ def _simultaneous(S, scorenet, sigmas, min_step, setting, n_steps_each, step_lr,
     return images, [], shared
 
 
+def view_blocks(n_all, world):
+    """[(v0, count)] per rank: the contiguous view block each rank of a view-split megabatch owns --
+    the first n_all % world ranks take one view more (the reference's DataParallel scatters its batch
+    in ceil-sized chunks, runners/ncsn_runner_kitti_simultaneous.py:481; any contiguous split merges
+    the same views)."""
+    base, extra = divmod(int(n_all), int(world))
+    return [(r * base + min(r, extra), base + (1 if r < extra else 0)) for r in range(world)]
+
+
 def _shard_setup(x_mod, actualBatchSize, view_shard):
-    """(n_all, own0): the views this call's buffers hold and where this rank's start."""
+    """(n_all, own0, blocks): the views this call's buffers hold, where this rank's start, and every
+    rank's (first view, count) -- None without a view shard."""
     B = x_mod.shape[0]
     if view_shard is None:
-        return B, 0
+        return B, 0, None
     rank, world = view_shard
-    if B * world != actualBatchSize:
-        raise ValueError("view_shard: each rank must hold actualBatchSize / world views of ONE megabatch")
-    return B * world, rank * B
+    blocks = view_blocks(actualBatchSize, world)
+    if blocks[-1][1] == 0:
+        raise ValueError("view_shard: a megabatch of actualBatchSize views cannot give every one of the world ranks a view")
+    if B != blocks[rank][1]:
+        raise ValueError(f"view_shard: rank {rank} of {world} must hold views [{blocks[rank][0]}, "
+                         f"{blocks[rank][0] + blocks[rank][1]}) of ONE megabatch of {actualBatchSize}, got {B}")
+    return actualBatchSize, blocks[rank][0], blocks
 
 
 @torch.no_grad()
@@ -246,8 +276,9 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti(
     toWorld, ``all_sky`` and ``all_refer_mask`` describe every view of the megabatch.
     """
     ops = ops or DeviceOps()
-    n_all, own0 = _shard_setup(x_mod, actualBatchSize, view_shard)
+    n_all, own0, blocks = _shard_setup(x_mod, actualBatchSize, view_shard)
     S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0, noise_views)
+    S.blocks = blocks
     sky_all = sky if view_shard is None else all_sky
     mask_all = S.mask if view_shard is None else all_refer_mask
     merger = ops.make_merger(n_all, actualBatchSize, S.H, S.W, S.dev, existMask, sky_all, mask_all, toWorld=toWorld,
@@ -273,8 +304,9 @@ def anneal_Langevin_dynamics_inpainting_simultaneous_basic(
         all_refer_mask=None, all_sky=None, ops=None, noise_views=None):
     """Origin-offset (AllForOne) simultaneous sampler (models/__init__.py:112-602)."""
     ops = ops or DeviceOps()
-    n_all, own0 = _shard_setup(x_mod, actualBatchSize, view_shard)
+    n_all, own0, blocks = _shard_setup(x_mod, actualBatchSize, view_shard)
     S = _Stepper(x_mod, refer_image, refer_mask, noise_fn, seed, ops, n_all, own0, noise_views)
+    S.blocks = blocks
     sky_all = sky if view_shard is None else all_sky
     mask_all = S.mask if view_shard is None else all_refer_mask
     origins = allforone_origins(modificationList)

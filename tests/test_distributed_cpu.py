@@ -1,10 +1,12 @@
-"""World-size-2 gloo test of the view-sharded simultaneous sampler (the multi-GPU path).
+"""gloo tests (world 2, 3 and 4) of the view-sharded simultaneous sampler (the multi-GPU path).
 
 Device ops are replaced by the CPU oracle (langevin / merge), and the score network by a
 cheap deterministic stand-in, so this checks exactly the sharding logic: per-rank views,
 the per-step all-gather of the megabatch, the all_reduce(MAX) that keeps tooHigh global,
 and each rank merging into its own views.  The sharded result must equal the single-process
-run bit for bit.
+run bit for bit.  World 4 has interior ranks (1, 2: neither first nor last block of the megabatch);
+world 3 over 8 views is an uneven split (3 + 3 + 2 views, the padded all-gather of
+sdp/sampling.py:_gather_views).
 """
 import os
 import socket
@@ -18,7 +20,7 @@ from oracle import golden_inputs as GI
 from oracle import philox_ref
 from oracle import sampling_ref as S
 
-B_ALL, H, W = 4, 64, 128
+B_ALL, H, W = 8, 64, 128
 SIGMAS = np.array([0.9, 0.6, 0.3], np.float32)
 
 
@@ -83,12 +85,14 @@ def _inputs():
 
 def _run(rank, world, port, out_dir, philox=False):
     from sdp.sampling import anneal_Langevin_dynamics_inpainting_simultaneous_basic_kitti as samp
+    from sdp.sampling import view_blocks
+    torch.set_num_threads(1)
     if world > 1:
         torch.distributed.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                                              world_size=world)
     case, x0 = _inputs()
-    Bl = B_ALL // world
-    sl = slice(rank * Bl, (rank + 1) * Bl)
+    v0, nv = view_blocks(B_ALL, world)[rank]
+    sl = slice(v0, v0 + nv)
     k = [0]
 
     def noise_fn(shape):  # slice of the single-process noise stream
@@ -116,15 +120,25 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("philox", [False, True], ids=["injected_noise", "philox_noise"])
-def test_view_sharded_sampler_matches_single_process(tmp_path, philox):
+def test_view_blocks_tile_the_megabatch():
+    from sdp.sampling import view_blocks
+    for n in range(1, 33):
+        for w in range(1, n + 1):
+            bl = view_blocks(n, w)
+            assert [v for v0, c in bl for v in range(v0, v0 + c)] == list(range(n))
+            assert max(c for _, c in bl) - min(c for _, c in bl) <= 1
+
+
+@pytest.mark.parametrize("world,philox", [(2, False), (2, True), (4, True), (3, True)],
+                         ids=["w2_injected_noise", "w2_philox_noise", "w4_interior_ranks", "w3_uneven_split"])
+def test_view_sharded_sampler_matches_single_process(tmp_path, world, philox):
     """philox_noise: no noise_fn, so each rank draws the kernel's own counter-based stream; the
     sharded run must draw the single-process noise for its views (counter offset = first view)."""
     _run(0, 1, 0, str(tmp_path), philox)
-    mp.spawn(_run, args=(2, _free_port(), str(tmp_path), philox), nprocs=2, join=True)
+    mp.spawn(_run, args=(world, _free_port(), str(tmp_path), philox), nprocs=world, join=True)
     sfx = "_p" if philox else ""
     single = np.load(tmp_path / f"w1_r0{sfx}.npy")                 # [n_images, B_ALL, 2, H, W]
-    shard = np.concatenate([np.load(tmp_path / f"w2_r{r}{sfx}.npy") for r in range(2)], axis=1)
+    shard = np.concatenate([np.load(tmp_path / f"w{world}_r{r}{sfx}.npy") for r in range(world)], axis=1)
     assert single.shape == shard.shape
     np.testing.assert_array_equal(shard, single)
     assert np.abs(single[-1] - GI.scorenet_input("dist", B_ALL, H, W)).max() > 1e-3   # the sampler did move x

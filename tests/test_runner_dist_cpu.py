@@ -1,6 +1,8 @@
 """main.py under torchrun: the sampling runner splits every batch's megabatches across ranks
 (replacing the reference's DataParallel, runners/ncsn_runner_kitti_simultaneous.py:481), and the
-files rank 0 writes must equal a single-process run bit for bit.  gloo world 2 on CPU; the device
+files rank 0 writes must equal a single-process run bit for bit.  gloo world 2 and 4 on CPU (3
+megabatches per batch: 2 + 1 at world 2; at world 4 ranks 1 and 2 are interior and rank 3 holds no
+megabatch, so it idles outside the active group that keeps tooHigh global); the device
 ops are the CPU oracle (Langevin update with the kernel's Philox noise stream, merge), the score
 network a cheap deterministic stand-in -- so this checks exactly the split: contiguous megabatch
 blocks, global tooHigh over the active ranks, per-view noise counters, the gather to rank 0."""
@@ -61,13 +63,14 @@ def test_shard_megabatches_covers_every_megabatch_once():
             assert got == list(range(n))
 
 
-@pytest.mark.parametrize("cfg", ["HDVMine_Line.yml", "HDVMine_Circle.yml"])
-def test_sharded_runner_writes_the_single_process_files(tmp_path, cfg):
-    one, two = tmp_path / "w1", tmp_path / "w2"
+@pytest.mark.parametrize("cfg,world", [("HDVMine_Line.yml", 2), ("HDVMine_Circle.yml", 2), ("HDVMine_Line.yml", 4),
+                                       ("HDVMine_Circle.yml", 4)])
+def test_sharded_runner_writes_the_single_process_files(tmp_path, cfg, world):
+    one, two = tmp_path / "w1", tmp_path / f"w{world}"
     one.mkdir()
     two.mkdir()
     _run(0, 1, 0, cfg, str(one))
-    mp.spawn(_run, args=(2, _port(), cfg, str(two)), nprocs=2, join=True)
+    mp.spawn(_run, args=(world, _port(), cfg, str(two)), nprocs=world, join=True)
     names = sorted(f for f in os.listdir(one) if f.endswith(".npy") and "TimeTaken" not in f)
     assert names and names == sorted(f for f in os.listdir(two) if f.endswith(".npy") and "TimeTaken" not in f)
     assert any("Masked_completion" in f for f in names)
