@@ -57,16 +57,21 @@ def min_depth_threshold(smod) -> np.float32:
     return F32(F32(l2 / F32(6)) * F32(smod))
 
 
-def _bin(q, g):
-    """Project relative points q [3,N] (float64) -> (row, col, logdepth-code before *smod)."""
+def _bin(q, g, raw=False):
+    """Project relative points q [3,N] (float64) -> (row, col, logdepth-code before *smod); with
+    raw=True also the unrounded bin coordinates (col, row) before rint."""
     xy = q[0] * q[0] + q[1] * q[1]
     d = np.sqrt(xy + q[2] * q[2])
     h = np.arctan2(q[1], q[0])
     e = np.arctan2(q[2], np.sqrt(xy))
-    col = np.rint((h - g["hMin"]) / g["hA"])
-    row = np.rint((e - g["bigMin"]) / g["vA"])
+    fc = (h - g["hMin"]) / g["hA"]
+    fr = (e - g["bigMin"]) / g["vA"]
+    col = np.rint(fc)
+    row = np.rint(fr)
     col = (g["W"] - 1 - col)
     row = (g["big"] - 1 - row)
+    if raw:
+        return row, col, d, fc, fr
     return row, col, d
 
 
@@ -135,13 +140,108 @@ def _apply(x, new, maskimg, sky, refmask, too_high, cc):
     return (x + F32(cc) * corr).astype(np.float32)
 
 
+
+# ----------------------------------------------------------------------------- parity flags
+# "exact mask and row/col bins; ties excluded".  A device merge computes the same
+# float64 projection from the same float32 image, except that its float32 exp2 (the real distance,
+# KITTISampling.py:164-166) may differ from the correctly rounded one by an ulp of 2^v and its float64
+# atan2 by an ulp.  flag_cells marks every destination cell whose result such a perturbation can
+# change: a point whose (row, col, validity) moves when its real distance moves by 2 ulp of (rd + 1)
+# either way, or whose bin coordinate sits within 1e-9 of a rounding edge; a nearest-depth tie (the
+# runner-up's code interval reaches the winner's); and a controlled-average branch
+# (KITTISampling.py:306-326) that the code intervals can flip.  Everywhere else a device merge must
+# agree exactly in its mask and within float rounding in its values (tests/test_gpu_parity.py).
+RD_ULPS = 2.0
+
+
+def _rd_perturbed(rd32):
+    """(rd - delta, rd + delta) in float64, delta = RD_ULPS ulp of float32(rd + 1) (the exp2 result)."""
+    rd = rd32.astype(np.float64)
+    dl = RD_ULPS * np.spacing(np.abs(rd32).astype(F32) + F32(1)).astype(np.float64)
+    mag = np.abs(rd)
+    sgn = np.where(rd < 0, -1.0, 1.0)
+    return sgn * np.maximum(mag - dl, 0.0), sgn * (mag + dl)
+
+
+def _cells_of(row, col, valid, g):
+    return (row[valid].astype(np.int64) * g["W"] + col[valid].astype(np.int64))
+
+
+def flag_cells(proj, smod, allowance, controlled, thr, extra_valid, g):
+    """Uncertain destination cells of one output view.  proj(k) -> (row, col, d, fc, fr) of every source
+    point for the nominal (k = 0), lowered (1) and raised (2) real distances; extra_valid: the
+    geometry-free validity (exist / sky).  Returns a bool [big * W] grid."""
+    W, big = g["W"], g["big"]
+    cells = big * W
+    ev = []
+    for k in range(3):
+        row, col, d, fc, fr = proj(k)
+        ell = np.log2(d + 1) / 6 * np.float64(smod)
+        valid = (col > -1) & (col < W) & (row > -1) & (row < big) & extra_valid
+        if thr is not None:
+            valid &= ell > thr
+        ev.append((row, col, ell, valid, fc, fr))
+    (r0, c0, l0, v0, fc0, fr0), (r1, c1, l1, v1, _, _), (r2, c2, l2, v2, _, _) = ev
+    edge = (np.abs(fc0 - np.floor(fc0) - 0.5) < 1e-9) | (np.abs(fr0 - np.floor(fr0) - 0.5) < 1e-9)
+    moved = (v0 != v1) | (v0 != v2) | (v0 & ((r0 != r1) | (c0 != c1) | (r0 != r2) | (c0 != c2))) | edge
+    flag = np.zeros(cells, bool)
+    for row, col, _, valid, _, _ in ev:
+        m = moved & valid
+        flag[_cells_of(row, col, m, g)] = True
+    # code intervals of the points that stay in their cell
+    lo, hi = np.minimum(np.minimum(l0, l1), l2), np.maximum(np.maximum(l0, l1), l2)
+    v = v0
+    idx = _cells_of(r0, c0, v, g)
+    lv, lov, hiv = l0[v], lo[v], hi[v]
+    n = np.bincount(idx, minlength=cells)
+    # nearest-depth ties: the runner-up (by nominal code) reaches the winner's interval
+    order = np.lexsort((np.arange(idx.size), lv, idx))
+    si = idx[order]
+    first = np.ones(order.size, bool)
+    first[1:] = si[1:] != si[:-1]
+    second = np.zeros(order.size, bool)
+    second[1:] = (~first[1:]) & first[:-1]
+    win = order[np.flatnonzero(second) - 1]
+    run = order[second]
+    tie = lov[run] <= hiv[win]
+    flag[idx[run][tie]] = True
+    if controlled:
+        scaling = (n.astype(np.float32) + F32(1e-9)).astype(np.float64)
+        a_lo = np.bincount(idx, weights=lov, minlength=cells) / scaling
+        a_hi = np.bincount(idx, weights=hiv, minlength=cells) / scaling
+        m_lo = np.zeros(cells)
+        m_hi = np.zeros(cells)
+        wsel = order[first]
+        m_lo[idx[wsel]] = lov[wsel]
+        m_hi[idx[wsel]] = hiv[wsel]
+        sm = np.float64(F32(smod))
+        f = lambda c: np.power(2.0, np.abs(c) * 6 / sm) - 1
+        c_hi = f(a_hi) > f(m_lo) + allowance      # the branch at its most likely...
+        c_lo = f(a_lo) > f(m_hi) + allowance      # ...and least likely ends
+        a0 = np.bincount(idx, weights=lv, minlength=cells) / scaling    # nominal (summation order aside)
+        m0 = np.zeros(cells)
+        m0[idx[wsel]] = lv[wsel]
+        edge = np.abs(f(a0) - (f(m0) + allowance)) <= 1e-9 * (f(m0) + allowance)
+        flag |= (n > 0) & ((c_hi != c_lo) | edge)
+    return flag
+
+
+def _flag_pixels(cellflag, isneg_o, g):
+    """Output pixels that read a flagged cell (the crop / flip of _crop_flip)."""
+    z = np.zeros(cellflag.shape, np.float32)
+    _, _, fl = _crop_flip(z, z, cellflag, isneg_o, g)
+    return fl
+
+
 def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5, allowance=10, cc=0.01,
-                absmax=None, views=None):
+                absmax=None, views=None, flags=False):
     """One consistency merge of the pose-matrix sampler (KITTISampling.py:160-490).
 
     x f32 [B,2,H,W] (after the Langevin update); returns (newImages f32, x corrected f32).
     absmax: max|x[:,0]| over every view of the step when x holds only some of them.
     views: compute only these output views (the others come back unmerged) -- large megabatches.
+    flags: also return the bool [B,H,W] pixels whose result a float-rounding perturbation of the
+    projection can change (flag_cells); the same pixels of the corrected x follow them.
     """
     B, _, H, W = x.shape
     g = merge_geometry(H, W)
@@ -150,21 +250,30 @@ def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5
     isneg = x0 < 0
     m = F32(np.abs(x0).max()) if absmax is None else F32(absmax)
     too_high = bool(F32(m * F32(6)) / F32(smod) > 50)
-    rd = real_distance(x0, smod).astype(np.float64)
+    rd32 = real_distance(x0, smod)
     caz, saz = np.cos(g["az"])[None, None, :], np.sin(g["az"])[None, None, :]
     cel, sel = np.cos(g["el"])[None, :, None], np.sin(g["el"])[None, :, None]
-    P = np.stack([(rd * caz * cel).reshape(B, -1), (rd * saz * cel).reshape(B, -1),
-                  (rd * sel).reshape(B, -1), np.ones((B, H * W))], 1)
-    Pw = np.einsum("bij,bjn->bin", toWorld, P)
+
+    def world(rd):
+        P = np.stack([(rd * caz * cel).reshape(B, -1), (rd * saz * cel).reshape(B, -1),
+                      (rd * sel).reshape(B, -1), np.ones((B, H * W))], 1)
+        return np.einsum("bij,bjn->bin", toWorld, P)
+    Pws = [world(rd32.astype(np.float64))]
+    if flags:
+        Pws += [world(r) for r in _rd_perturbed(rd32)]
     thr = np.float64(min_depth_threshold(smod))
     ex = exist[:aB].reshape(-1)
     new = np.zeros_like(x)
     maskimg = np.zeros((B, H, W), bool)
+    flagged = np.zeros((B, H, W), bool)
     for o in (range(B) if views is None else views):
         m0 = (o // aB) * aB
-        src = Pw[m0:m0 + aB]                                 # [aB,4,HW]
-        q = np.einsum("ij,vjn->vin", fromWorld[o], src)[:, :3].transpose(1, 0, 2).reshape(3, -1)
-        row, col, d = _bin(q, g)
+
+        def proj(k, raw=False):
+            src = Pws[k][m0:m0 + aB]                          # [aB,4,HW]
+            q = np.einsum("ij,vjn->vin", fromWorld[o], src)[:, :3].transpose(1, 0, 2).reshape(3, -1)
+            return _bin(q, g, raw)
+        row, col, d = proj(0)
         ell = np.log2(d + 1) / 6 * np.float64(smod)
         valid = (col > -1) & (col < W) & (row > -1) & (row < g["big"]) & ex
         if setting == 5:
@@ -176,7 +285,11 @@ def kitti_merge(x, refmask, sky, exist, toWorld, fromWorld, aB, sigma, setting=5
         new[o, 0] = dep.astype(np.float32)
         new[o, 1] = inn
         maskimg[o] = np.logical_and(exist[0], cmask)
-    return new, _apply(x, new, maskimg, sky, refmask, too_high, cc)
+        if flags:
+            cf = flag_cells(lambda k: proj(k, True), smod, allowance, True, thr if setting == 5 else None, ex, g)
+            flagged[o] = _flag_pixels(cf, isneg[o], g)
+    out = _apply(x, new, maskimg, sky, refmask, too_high, cc)
+    return (new, out, flagged) if flags else (new, out)
 
 
 def allforone_origins(mods) -> np.ndarray:
@@ -190,8 +303,9 @@ def allforone_origins(mods) -> np.ndarray:
     return ((o / den).astype(np.float32) * F32(10)).astype(np.float32)
 
 
-def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01, views=None, absmax=None):
-    """One merge of the origin-offset sampler (models/__init__.py:263-579).  absmax: as kitti_merge."""
+def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01, views=None, absmax=None,
+                    flags=False):
+    """One merge of the origin-offset sampler (models/__init__.py:263-579).  absmax, flags: as kitti_merge."""
     B, _, H, W = x.shape
     g = merge_geometry(H, W)
     smod = sigma_mod_of(sigma)
@@ -199,7 +313,8 @@ def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01,
     isneg = x0 < 0
     m = F32(np.abs(x0).max()) if absmax is None else F32(absmax)
     too_high = bool(F32(m * F32(6)) / F32(smod) > 50)
-    rd = real_distance(x0, smod).astype(np.float64)
+    rd32 = real_distance(x0, smod)
+    rds = [rd32.astype(np.float64)] + (list(_rd_perturbed(rd32)) if flags else [])
     org = allforone_origins(mods).astype(np.float64)[:aB]       # [aB,3]
     caz, saz = np.cos(g["az"])[None, None, :], np.sin(g["az"])[None, None, :]
     cel, sel = np.cos(g["el"])[None, :, None], np.sin(g["el"])[None, :, None]
@@ -208,18 +323,22 @@ def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01,
     allowance = 5 if setting >= 8 else 10
     new = np.zeros_like(x)
     maskimg = np.zeros((B, H, W), bool)
+    flagged = np.zeros((B, H, W), bool)
     for o in (range(B) if views is None else views):
         m0 = (o // aB) * aB
-        r = rd[m0:m0 + aB]
-        px = (r * caz * cel + org[:, 0, None, None]).reshape(-1)
-        py = (r * saz * cel + org[:, 1, None, None]).reshape(-1)
-        pz = (r * sel + org[:, 2, None, None]).reshape(-1)
         oo = org[o - m0]
-        q = np.stack([px - oo[0], py - oo[1], pz - oo[2]])
-        row, col, d = _bin(q, g)
+
+        def proj(k, raw=False):
+            r = rds[k][m0:m0 + aB]
+            px = (r * caz * cel + org[:, 0, None, None]).reshape(-1)
+            py = (r * saz * cel + org[:, 1, None, None]).reshape(-1)
+            pz = (r * sel + org[:, 2, None, None]).reshape(-1)
+            return _bin(np.stack([px - oo[0], py - oo[1], pz - oo[2]]), g, raw)
+        row, col, d = proj(0)
         ell = np.log2(d + 1) / 6 * np.float64(smod)
         valid = (col > -1) & (col < W) & (row > -1) & (row < g["big"])
-        valid &= sky[m0:m0 + aB].reshape(-1) & ex & (ell > thr)
+        geo_free = sky[m0:m0 + aB].reshape(-1) & ex
+        valid &= geo_free & (ell > thr)
         inten = x[m0:m0 + aB, 1].reshape(-1)
         acc = _accumulate(row, col, ell, inten, valid, g)
         code, I, cm = _resolve(*acc, smod, allowance, controlled=setting >= 7)
@@ -227,7 +346,11 @@ def allforone_merge(x, refmask, sky, exist, mods, aB, sigma, setting=7, cc=0.01,
         new[o, 0] = dep.astype(np.float32)
         new[o, 1] = inn
         maskimg[o] = np.logical_and(exist[0], cmask)
-    return new, _apply(x, new, maskimg, sky, refmask, too_high, cc)
+        if flags:
+            cf = flag_cells(lambda k: proj(k, True), smod, allowance, setting >= 7, thr, geo_free, g)
+            flagged[o] = _flag_pixels(cf, isneg[o], g)
+    out = _apply(x, new, maskimg, sky, refmask, too_high, cc)
+    return (new, out, flagged) if flags else (new, out)
 
 
 # ----------------------------------------------------------------------------- Langevin

@@ -49,10 +49,6 @@ def _absmax(x):
     return torch.tensor([np.abs(x[:, 0]).max()], dtype=torch.float32).view(torch.int32).to(DEV)
 
 
-def _close_frac(a, b, rtol=1e-5, atol=2e-6):
-    return np.mean(np.abs(a - b) > atol + rtol * np.abs(b))
-
-
 def test_rank_local_merge_equals_full_merge_and_golden(case):
     x0 = _after_update(case)
     full_x = torch.from_numpy(x0).to(DEV)
@@ -77,8 +73,12 @@ def test_rank_local_merge_equals_full_merge_and_golden(case):
                 seen[v] = new[v - o_begin]
     assert sorted(seen) == sorted(golden_views)
     got = np.stack([seen[v] for v in golden_views])
-    assert _close_frac(got, f["new"]) <= 1e-4
-    assert np.mean((got != 0) != (f["new"] != 0)) <= 1e-4
+    from oracle import sampling_ref as S
+    from test_gpu_parity import _assert_merge_exact
+    _, _, fl = S.kitti_merge(x0, case["mask"], case["sky"], case["exist"], case["toWorld"], case["fromWorld"], N_SRC,
+                             0.5, views=golden_views, flags=True)
+    gx = (full_x + (-case["mask"]).astype(np.float32) * (full_x - case["ref"])).astype(np.float32)[golden_views]
+    _assert_merge_exact(got, f["new"], gx, f["x"], fl[golden_views], "config-4 rank-local")
 
 
 def test_eight_rank_viewsplit_emulation_is_bit_identical(case):

@@ -5,9 +5,11 @@ Tolerances (stated once, used below):
   * score net, fp32 (exact fp32 MFMA):           max|err| <= 2e-5 * max|ref| per image
   * Langevin update: bit-exact (same float32 ops and order, injected noise); the update fused
     into the score net's last kernel: bit-identical to the two-call form
-  * merge: new images / corrected x within rtol 1e-5, atol 2e-6 on all but <= 1e-4 of the
-    pixels (float64 atan2/log2 of the GPU vs glibc can move a point sitting exactly on a
-    bin edge); the known/unknown mask pattern must agree on the same fraction.
+  * merge (exact mask and bins, ties excluded): the oracle flags the pixels whose
+    result a float-rounding perturbation of the projection can change (a point within rounding of a
+    bin edge or of the depth filter, a nearest-depth tie, a controlled-average branch on its edge;
+    oracle/sampling_ref.py flag_cells); everywhere else the zero pattern must agree exactly and the
+    new images / corrected x within rtol 1e-5, atol 2e-6 -- no fraction of mismatches allowed.
 """
 import os
 
@@ -251,15 +253,34 @@ def _close_frac(a, b, rtol=1e-5, atol=2e-6):
     return np.mean(np.abs(a - b) > atol + rtol * np.abs(b))
 
 
+def _assert_merge_exact(got_new, want_new, got_x, want_x, flagged, what=""):
+    """SURVEY 8(c) merge gate: outside the pixels the oracle flags (oracle/sampling_ref.py flag_cells:
+    a point within float rounding of a bin edge or of the depth filter, a nearest-depth tie, a
+    controlled-average branch on its edge) the zero pattern (mask / bins) must agree exactly and every
+    value within float rounding (rtol 1e-5, atol 2e-6: float64 sums in another order, the device's float32
+    exp2); no fraction of mismatches is allowed.  Prints the flagged count."""
+    fl = np.broadcast_to(np.asarray(flagged)[:, None], got_new.shape)
+    ok = ~fl
+    bad_new = (np.abs(got_new - want_new) > 2e-6 + 1e-5 * np.abs(want_new)) & ok
+    bad_zero = ((got_new != 0) != (want_new != 0)) & ok
+    bad_x = (np.abs(got_x - want_x) > 2e-6 + 1e-5 * np.abs(want_x)) & ok
+    print(f"merge {what}: {int(np.asarray(flagged).sum())} of {np.asarray(flagged).size} pixels flagged, "
+          f"mismatches outside them: values {int(bad_new.sum())}, zero pattern {int(bad_zero.sum())}, x {int(bad_x.sum())}")
+    assert np.asarray(flagged).mean() <= 2e-3, "the oracle flags too much to grade"
+    assert not bad_zero.any(), np.argwhere(bad_zero)[:8]
+    assert not bad_new.any(), np.argwhere(bad_new)[:8]
+    assert not bad_x.any(), np.argwhere(bad_x)[:8]
+
+
 @pytest.mark.parametrize("case_def", MERGE_CASES, ids=[c[0] for c in MERGE_CASES])
 def test_kitti_merge_matches_reference_golden(case_def):
     tag, B, aB, H, W, sigma, kw = case_def
     case = GI.merge_case(tag, B, H, W, **kw)
     f = _g(f"merge_{tag}.npz")
     new, xc = _gpu_merge(case, aB, sigma, 5, 10, 0.01)
-    assert _close_frac(new, f["new"]) <= 1e-4
-    assert _close_frac(_final_dc(xc, case), f["x"]) <= 1e-4
-    assert np.mean((new != 0) != (f["new"] != 0)) <= 1e-4
+    _, _, fl = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                             case["fromWorld"], aB, sigma, flags=True)
+    _assert_merge_exact(new, f["new"], _final_dc(xc, case), f["x"], fl, tag)
 
 
 @pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5), ("a_b7_s05_set8", 8)])
@@ -272,8 +293,9 @@ def test_allforone_merge_matches_reference_golden(tag, setting):
     cc = 1.0 if setting == 5 else 0.01
     allowance = 5 if setting >= 8 else 10
     new, xc = _gpu_merge(case, 7, 0.5, setting, allowance, cc, origins=allforone_origins(CIRCLE_MODS))
-    assert _close_frac(new, f["new"]) <= 1e-4
-    assert _close_frac(_final_dc(xc, case), f["x"]) <= 1e-4
+    _, _, fl = S.allforone_merge(_after_update(case), case["mask"], case["sky"], case["exist"], CIRCLE_MODS, 7, 0.5,
+                                 setting, cc, flags=True)
+    _assert_merge_exact(new, f["new"], _final_dc(xc, case), f["x"], fl, tag)
 
 
 def test_allforone9_merge_matches_reference_golden():
@@ -283,8 +305,9 @@ def test_allforone9_merge_matches_reference_golden():
     case = GI.merge_case("a_b9_s05_set7", 9, 64, 256)
     f = _g("merge_a_b9_s05_set7.npz")
     new, xc = _gpu_merge(case, 9, 0.5, 7, 10, 0.01, origins=allforone_origins(CIRCLE9))
-    assert _close_frac(new, f["new"]) <= 1e-4
-    assert _close_frac(_final_dc(xc, case), f["x"]) <= 1e-4
+    _, _, fl = S.allforone_merge(_after_update(case), case["mask"], case["sky"], case["exist"], CIRCLE9, 9, 0.5, 7,
+                                 0.01, flags=True)
+    _assert_merge_exact(new, f["new"], _final_dc(xc, case), f["x"], fl, "a_b9_s05_set7")
 
 
 def test_megabatch32_full_width_matches_reference_golden():
@@ -293,9 +316,9 @@ def test_megabatch32_full_width_matches_reference_golden():
     f = _g("merge_k_b32a32_full.npz")
     v = list(f["views"])
     new, xc = _gpu_merge(case, 32, 0.5, 5, 10, 0.01)
-    assert _close_frac(new[v], f["new"]) <= 1e-4
-    assert _close_frac(_final_dc(xc, case)[v], f["x"]) <= 1e-4
-    assert np.mean((new[v] != 0) != (f["new"] != 0)) <= 1e-4
+    _, _, fl = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                             case["fromWorld"], 32, 0.5, views=v, flags=True)
+    _assert_merge_exact(new[v], f["new"], _final_dc(xc, case)[v], f["x"], fl[v], "k_b32a32_full")
 
 
 def test_merge_too_high_disables_correction():
@@ -308,10 +331,9 @@ def test_merge_megabatch8_w512_vs_oracle():
     """aB=8 (more views than any golden) against the oracle restatement."""
     case = GI.merge_case("big8", 8, 64, 512)
     new, xc = _gpu_merge(case, 8, 0.7, 5, 10, 0.01)
-    on, ox = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
-                           case["fromWorld"], 8, 0.7)
-    assert _close_frac(new, on) <= 1e-4
-    assert _close_frac(xc, ox) <= 1e-4
+    on, ox, fl = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                               case["fromWorld"], 8, 0.7, flags=True)
+    _assert_merge_exact(new, on, xc, ox, fl, "big8")
 
 
 @pytest.mark.parametrize("aB,W", [(16, 256), (32, 128)])
@@ -320,10 +342,9 @@ def test_merge_large_megabatch_vs_oracle(aB, W):
     accumulation sums many 4096-record segments per destination row, against the oracle."""
     case = GI.merge_case(f"big{aB}", aB, 64, W)
     new, xc = _gpu_merge(case, aB, 0.7, 5, 10, 0.01)
-    on, ox = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
-                           case["fromWorld"], aB, 0.7)
-    assert _close_frac(new, on) <= 1e-4
-    assert _close_frac(xc, ox) <= 1e-4
+    on, ox, fl = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                               case["fromWorld"], aB, 0.7, flags=True)
+    _assert_merge_exact(new, on, xc, ox, fl, f"big{aB}")
 
 
 def _noise_feed(tag):
