@@ -15,6 +15,7 @@
 // to the output view, and an apply pass adds cc * (-mask*(x - new)) on unknown pixels
 // unless tooHigh.  Tie rule: equal nearest codes keep the lowest source index (the
 // reference's unstable argsort leaves it unspecified).
+#include <mutex>
 #include "merge.h"
 
 // reference evaluation order: no FMA contraction in this file (HIP __fmul_rn is a plain `*`)
@@ -186,7 +187,10 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
 
 // The top level of the offset scan rides here (one launch less): every workgroup scans the nb block
 // totals of merge_scan_block_kernel in LDS; workgroup 0 also publishes every tile's first record and
-// the total (toff) for the segment passes, which run after this launch.
+// the total (toff) for the segment passes, which run after this launch.  The scan is redundant work:
+// each of the nchunk workgroups reads all nb totals from L2 (nchunk * nb loads, at most 1024 x 8192) --
+// cheaper than the launch it replaces at the measured sizes (4 views: 156 -> 110 us for the whole chain,
+// a 32-view config-4 rank 401 -> 352 us; profiles/experiments/r05_merge_chain_ab.log).
 __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, size_t per_chunk, int nb) {
   extern __shared__ uint32_t cur[];                // [T] tile cursors, then [nb + 1] scanned block totals
   const int HW = a.g.H * a.g.W, T = a.n_out * a.g.big, tid = threadIdx.x;
@@ -386,6 +390,11 @@ __global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a) {
 // image, then -- unless tooHigh (KITTISampling.py:162) -- x += cc * -(x - new) on the unknown pixels
 // of both channels.  The nearest point's intensity comes from the snapshot taken before any pixel is
 // corrected; a pixel's own depth sign is read before the pass writes it.
+// Trade-off of the fusion: with a multi-rank tooHigh (apply_wait) the whole pass, resolve included,
+// now waits for the all_reduce(MAX) event, where the two-launch form ran the resolve beside it; the
+// all_reduce of one word (<= ~20 us over xGMI) is issued right after the Langevin update and overlaps
+// the five binning / segment launches before this one, so the wait is empty unless the collective is
+// slower than that whole chain.
 __global__ __launch_bounds__(256) void merge_resolve_apply_kernel(MergeArgs a) {
   const int H = a.g.H, W = a.g.W, HW = H * W;
   const int cells = a.g.big * W;
@@ -508,27 +517,39 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   a.isnap = reinterpret_cast<float*>(take(nw * 4));
   a.toff = reinterpret_cast<uint32_t*>(take(((size_t)T + 1) * 4));
   const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
+  // dynamic LDS of each launch, checked against the per-workgroup limit BEFORE anything is enqueued:
+  // count = the tile histogram [T]; scatter = the tile cursors [T] + the scanned block totals [nb + 1]
+  // beside its 1 KB static scan array; segment passes = the tile table [T + 1] beside 57 KB static
   const size_t lds = (size_t)T * 4;
-  if (lds + ((size_t)nb + 1) * 4 > 64 * 1024) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
+  const size_t slds = lds + ((size_t)nb + 1) * 4;
+  const size_t tlds = ((size_t)T + 1) * 4;
+  constexpr size_t kDyn = 96 * 1024;   // the attribute set below (<= 160 KB per CU on gfx950)
+  if (lds > kDyn) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
+  if (slds + 1024 > kDyn) { *why = "merge: too many output views x chunks for the scatter's cursor + scan tables"; return hipErrorInvalidValue; }
+  if (tlds + 57 * 1024 > 152 * 1024) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
   hipError_t e;
+  // the max-dynamic-LDS attribute acts on the current device: set once per device (thread-safe)
+  {
+    static std::mutex mu;
+    static uint64_t done = 0;   // bit d: device d configured
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(mu);
+    if (dev >= 64 || !((done >> dev) & 1u)) {
+      const void* fns[] = {(const void*)merge_bin_count_kernel, (const void*)merge_bin_scatter_kernel,
+                           (const void*)merge_seg_sum_kernel, (const void*)merge_seg_minidx_kernel};
+      for (const void* f : fns)
+        if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDyn)) != hipSuccess) return e;
+      if (dev < 64) done |= 1ull << dev;
+    }
+  }
   // seven dependent launches: world (+ grid reset, intensity snapshot) -> count -> block scan ->
   // scatter (+ top scan, tile table) -> segment sums -> nearest index -> resolve + correction
   hipLaunchKernelGGL(merge_world_kernel, dim3(grid_for(std::max(nw, (size_t)a.n_out * cells))), dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_bin_count_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
   hipLaunchKernelGGL(merge_scan_block_kernel, dim3(nb), dim3(256), 0, st, a.tcount, nt, a.bsum);
-  hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), lds + ((size_t)nb + 1) * 4, st, a, per_chunk, nb);
+  hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), slds, st, a, per_chunk, nb);
   const int nseg = (int)((npair + MERGE_SEG - 1) / MERGE_SEG);   // upper bound: records <= pairs
-  const size_t tlds = ((size_t)T + 1) * 4;
-  static bool lds_attr = false;   // the tile table beside the segment passes' 57 KB of static LDS
-  if (!lds_attr) {
-    if ((e = hipFuncSetAttribute((const void*)merge_seg_sum_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 96 * 1024)) != hipSuccess ||
-        (e = hipFuncSetAttribute((const void*)merge_seg_minidx_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 96 * 1024)) != hipSuccess)
-      return e;
-    lds_attr = true;
-  }
-  if (tlds > 96 * 1024) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
   hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), tlds, st, a);
   hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), tlds, st, a);
   if (apply_wait && (e = hipStreamWaitEvent(st, apply_wait, 0)) != hipSuccess) return e;   // tooHigh's global max

@@ -520,11 +520,19 @@ int wgrad_splits(int B, int H, int W, int d, int Cin, int Cout, int ks) {
 
 size_t wgrad_part_floats(int S, int Cin, int Cout, int ks) { return (size_t)S * ks * ks * Cin * Cout; }
 
+// tc: the tile width of the 3x3 launches (64 -> 2 x 64 tiles, 32 -> 4 x 32).  OCC 3 has no 2 x 64
+// instantiation (its double-buffered dy tile does not fit twice per CU), so it runs 4 x 32 tiles
+// whatever tc says -- wgrad_mode passes 32 for it.
 template <int MODE, int OCC>
 static hipError_t wgrad_occ(const WgradArgs& a, int ks, int tc, dim3 grid, hipStream_t st) {
+  static_assert(OCC >= 1 && OCC <= 3, "wgrad: OCC 1, 2 or 3");
   if (ks == 1) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 1, OCC>), grid, dim3(256), 0, st, a);
-  else if (tc == 64 && OCC != 3) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3, OCC == 3 ? 2 : OCC>), grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3, OCC>), grid, dim3(256), 0, st, a);
+  else if constexpr (OCC != 3) {
+    if (tc == 64) hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 64, 3, OCC>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3, OCC>), grid, dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((conv_wgrad_kernel<MODE, 32, 3, OCC>), grid, dim3(256), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -542,7 +550,7 @@ template <int MODE>
 static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStream_t st) {
   dim3 grid(S * (a.Cin / 32) * (a.Cout / 128));
   if constexpr (MODE == MODE_BF16) {
-    if (SDP_WGRAD_OCC3) {
+    if (SDP_WGRAD_OCC3) {   // OCC 3 always runs 4 x 32 tiles for the 3x3 convs (the caller's tc is not used)
       const int Ws = a.W / a.dil, Hs = a.H / a.dil;
       if (ks == 1) return wgrad_occ<MODE, 3>(a, ks, tc, grid, st);
       if (Ws % 32 == 0 && Hs % 4 == 0) return wgrad_occ<MODE, 3>(a, ks, 32, grid, st);

@@ -347,6 +347,17 @@ def test_merge_large_megabatch_vs_oracle(aB, W):
     _assert_merge_exact(new, on, xc, ox, fl, f"big{aB}")
 
 
+def test_merge_near_the_output_view_limit_vs_oracle():
+    """140 output views (35 megabatches of 4) at 64 x 32: the scatter's LDS holds the tile cursors
+    (140 x 114 x 4 B) AND the scanned block totals (>= 4 K of them) -- past the old 64 KB check
+    (ADVICE r05), under the 96 KB attribute set per device; every view against the oracle."""
+    case = GI.merge_case("many140", 140, 64, 32)
+    new, xc = _gpu_merge(case, 4, 0.7, 5, 10, 0.01)
+    on, ox, fl = S.kitti_merge(_after_update(case), case["mask"], case["sky"], case["exist"], case["toWorld"],
+                               case["fromWorld"], 4, 0.7, flags=True)
+    _assert_merge_exact(new, on, xc, ox, fl, "140 views")
+
+
 def _noise_feed(tag):
     k = [0]
 
