@@ -83,6 +83,8 @@ def parse():
                     help="line/allforone: score net and Langevin update as two calls (sdp_net_forward + "
                          "sdp_langevin_step) instead of sdp_net_forward_langevin")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--fp32-tape", action="store_true",
+                    help="train workload, bf16: keep the training tape in float32 (A/B against the bf16 tape)")
     ap.add_argument("--sustained-s", type=float, default=3.0,
                     help="line/allforone: also time >= this many seconds of back-to-back steps after >= "
                          "--sustained-warm-s of warm load (the clock under MFMA load settles only after ~2 s; "
@@ -475,7 +477,7 @@ def run_train(args, rank, N, dist, dev):
 
     H, W, Bg = 64, 1024, args.views
     net = ScoreNet(H=H, W=W, precision=args.precision).load_synthetic()
-    tr = Trainer(net, lr=1e-4, dist_group=torch.distributed.group.WORLD if dist else None)
+    tr = Trainer(net, lr=1e-4, dist_group=torch.distributed.group.WORLD if dist else None, tape_bf16=not args.fp32_tape)
     sc = scene_views(Bg, H, W, seed=1234 + rank)
     X0 = torch.from_numpy(sc["ref"]).to(dev)
     mask = torch.from_numpy(sc["mask"]).to(dev).float()
@@ -511,7 +513,8 @@ def run_train(args, rank, N, dist, dev):
             "config": {"workload": "Densification.yml DSM training step (kitti runner loop body: fwd + masked DSM "
                                    "loss + backward + grad all-reduce + Adam + EMA + 5 Langevin predictions)",
                        "batch_per_gpu": Bg, "global_batch": Bg * N, "parallelism": f"dp{N}",
-                       "conv_arithmetic": args.precision},
+                       "conv_arithmetic": args.precision,
+                       "tape": "float32" if (args.fp32_tape or args.precision != "bf16") else "bf16"},
             "roofline": roof, "cpu_baseline": cpu, "final_loss": float(losses[-1])}
 
 

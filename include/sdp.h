@@ -123,6 +123,12 @@ int sdp_net_repack(sdp_net* net, void* stream);
  * d loss/d parameters for d loss/d out = dscore into `grads` (a parameter-layout arena,
  * overwritten) -- same workspace and B, no other train-mode call on this net in between.   */
 int sdp_net_train_workspace_size(sdp_net* net, int B, size_t* bytes);
+/* bf16 precision only: 1 (the default) keeps the tape -- every activation and output gradient of
+ * sdp_net_forward_train / sdp_net_backward -- in bf16 (half the bytes of every conv's operand and
+ * epilogue streams, of the weight gradient's and of the adjoints'); 0 keeps it in float32.  The
+ * parameters, the gradient arena, the statistics and the scores are float32 either way.  Takes effect
+ * at the next sdp_net_train_workspace_size / sdp_net_forward_train (the workspace size depends on it). */
+int sdp_net_set_tape(sdp_net* net, int bf16);
 int sdp_net_forward_train(sdp_net* net, const float* x, const int64_t* labels, float* out, int B,
                           void* workspace, size_t workspace_bytes, void* stream);
 int sdp_net_backward(sdp_net* net, const float* dscore, int B, void* workspace, size_t workspace_bytes,

@@ -201,11 +201,14 @@ SDP_DEV void bm_store(f32x4v v, f32x4v* p) {
 #ifndef SDP_HEAD_DIRECT   // A/B switch (tools/lib_variant.sh only): 1 = the direct fp32 begin/end conv in every mode
 #define SDP_HEAD_DIRECT 0
 #endif
-template <int MODE>
+SDP_DEV void bm_store(f32x4v v, __bf16* p) { *reinterpret_cast<uint2*>(p) = f4_to_bf4(make_float4(v[0], v[1], v[2], v[3])); }
+SDP_DEV void bm_store(f32x4v v, float* p) { bm_store(v, reinterpret_cast<f32x4v*>(p)); }
+// TO: the output's element type (__bf16 in the bf16 training tape, train.hip); statistics from the float values
+template <int MODE, typename TO = float>
 __global__ __launch_bounds__(256, BM_WG_PER_CU) void begin_conv_mfma_kernel(const float* __restrict__ x,
                                                                            const float* __restrict__ w,
                                                                            const float* __restrict__ bias,
-                                                                           float* __restrict__ out,
+                                                                           TO* __restrict__ out,
                                                                            float* __restrict__ stats, int B, int H, int W) {
   constexpr int CO = 128, NI = 6 * 130, PE = (NI + 255) / 256;
   __shared__ __attribute__((aligned(16))) float sp[12 * BC_RS];   // [ci*3 + row][col], cols -1 .. 128
@@ -323,9 +326,9 @@ __global__ __launch_bounds__(256, BM_WG_PER_CU) void begin_conv_mfma_kernel(cons
 #pragma unroll
     for (int i = 0; i < 16; ++i) tv[i] = *reinterpret_cast<const f32x4v*>(tw + (4 * i + pq) * BM_TS + 4 * c4);
     if constexpr (!(SDP_BM_KO & 1)) {
-      float* o = out + (((size_t)b * H + y) * W + x0 + 64 * ph + pq) * CO + 64 * ch + 4 * c4;
+      TO* o = out + (((size_t)b * H + y) * W + x0 + 64 * ph + pq) * CO + 64 * ch + 4 * c4;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) bm_store(tv[i], reinterpret_cast<f32x4v*>(o + (size_t)4 * i * CO));
+      for (int i = 0; i < 16; ++i) bm_store(tv[i], o + (size_t)4 * i * CO);
     }
     if constexpr (SDP_BM_KO & 2) continue;
     f32x4v mean = tv[0];
@@ -362,13 +365,12 @@ __global__ __launch_bounds__(256, BM_WG_PER_CU) void begin_conv_mfma_kernel(cons
 #else
     if constexpr (!(SDP_BM_KO & 1)) {
     // stores: lane = 4 channels (64 ch + 16 f + 4 q ..) of pixel x0 + 64 ph + 16 g + l16
-    float* o = out + (((size_t)b * H + y) * W + x0 + 64 * ph + l16) * CO + 64 * ch + 4 * q;
+    TO* o = out + (((size_t)b * H + y) * W + x0 + 64 * ph + l16) * CO + 64 * ch + 4 * q;
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
       for (int f = 0; f < 4; ++f)
-        bm_store(f32x4v{acc[g][f][0], acc[g][f][1], acc[g][f][2], acc[g][f][3]},
-                                    reinterpret_cast<f32x4v*>(o + (size_t)16 * g * CO + 16 * f));
+        bm_store(f32x4v{acc[g][f][0], acc[g][f][1], acc[g][f][2], acc[g][f][3]}, o + (size_t)16 * g * CO + 16 * f);
     }
     if constexpr (SDP_BM_KO & 2) continue;
     // statistics of this wave's 64-pixel group: 4 values per lane and channel, then the 16 lanes
@@ -556,8 +558,8 @@ constexpr int E2_NG = (E2_NP + 15) / 16, E2_PS = 19;   // 16-pixel groups; P row
 #ifndef SDP_EC_SS_LDS     // 1: IN++ (scale, shift) read from LDS per group; 0: held in registers
 #define SDP_EC_SS_LDS 0
 #endif
-template <int MODE, bool LGV>
-__global__ __launch_bounds__(256, 2) void end_conv_mfma_kernel(const float* __restrict__ in, const float* __restrict__ ss,
+template <int MODE, bool LGV, typename TI = float>
+__global__ __launch_bounds__(256, 2) void end_conv_mfma_kernel(const TI* __restrict__ in, const float* __restrict__ ss,
                                                                const float* __restrict__ w, const float* __restrict__ bias,
                                                                const float* __restrict__ sigmas,
                                                                const int64_t* __restrict__ labels, float* __restrict__ out,
@@ -575,7 +577,7 @@ __global__ __launch_bounds__(256, 2) void end_conv_mfma_kernel(const float* __re
   auto load_group = [&](int g, float4 (&r)[8]) __attribute__((always_inline)) {
     const int p = 16 * g + l16, pr = p / E2_PC, pc = p - pr * E2_PC;
     const int yy = min(max(y0 - 1 + pr, 0), H - 1), xx = min(max(x0 - 1 + pc, 0), W - 1);
-    const float* src = in + (((size_t)b * H + yy) * W + xx) * Cin + 4 * q;
+    const size_t src = (((size_t)b * H + yy) * W + xx) * Cin + 4 * q;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       if constexpr (SDP_EC_KO & 4) {
@@ -583,8 +585,8 @@ __global__ __launch_bounds__(256, 2) void end_conv_mfma_kernel(const float* __re
         r[2 * ks + 1] = r[2 * ks];
         continue;
       }
-      r[2 * ks] = *reinterpret_cast<const float4*>(src + 32 * ks);
-      r[2 * ks + 1] = *reinterpret_cast<const float4*>(src + 32 * ks + 16);
+      r[2 * ks] = ldg4(in, src + 32 * ks);
+      r[2 * ks + 1] = ldg4(in, src + 32 * ks + 16);
     }
   };
   float4 ra[8], rb[8];
@@ -944,11 +946,128 @@ __global__ __launch_bounds__(256) void maxpool5_kernel(const float* __restrict__
   __builtin_amdgcn_s_waitcnt(0x0f70);              // the rows landed past the strip's end
 }
 
+// maxpool 5x5 s1 p2 with the argmax indices on a bf16 tensor (the bf16 training tape, train.hip): the
+// same window order, tie rule and -inf padding as maxpool5_kernel<true>.  Block = 32 columns x 128
+// channels over `rows` output rows; thread (column xl, 8-channel group c8) owns column xl.
+// Each input row of the strip (+2 halo columns each side, out-of-image positions -inf) is read once into
+// an LDS slot (the next row's loads fly in registers while the current row is reduced), the horizontal
+// 5-max comes from LDS and slides down a 5-row register window
+constexpr int MPH_COLS = 16, MPH_SC = MPH_COLS + 4, MPH_U = MPH_SC * 16;   // staged 16-B units per row: 320
+__global__ __launch_bounds__(256) void maxpool5_h16_kernel(const __bf16* __restrict__ in, __bf16* __restrict__ out,
+                                                           unsigned char* __restrict__ idx, int B, int H, int W, int C,
+                                                           int rows) {
+  __shared__ uint4 srow[2][MPH_U];
+  const int tid = threadIdx.x, c8 = tid & 15, xl = tid >> 4;
+  const int CG = C / 128, strips = W / MPH_COLS, RB = (H + rows - 1) / rows;
+  int t = blockIdx.x;
+  const int cg = t % CG;
+  t /= CG;
+  const int strip = t % strips;
+  t /= strips;
+  const int rb = t % RB, b = t / RB;
+  const int x0 = strip * MPH_COLS, y0 = rb * rows, y1 = min(H, y0 + rows);
+  constexpr uint32_t NEG2 = 0xff80ff80u;           // two bf16 -inf
+  uint4 pre[2];
+  auto fetch = [&](int yy) {                        // row yy's units of this thread -> registers
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k, col = i >> 4, cc = i & 15, xx = x0 - 2 + col;
+      pre[k] = make_uint4(NEG2, NEG2, NEG2, NEG2);
+      if (i < MPH_U && yy >= 0 && yy < H && xx >= 0 && xx < W)
+        pre[k] = *reinterpret_cast<const uint4*>(in + (((size_t)b * H + yy) * W + xx) * C + cg * 128 + cc * 8);
+    }
+  };
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int i = tid + 256 * k;
+      if (i < MPH_U) srow[slot][i] = pre[k];
+    }
+  };
+  // horizontal 5-max (first max on ties) of column xl from LDS slot
+  auto hmax = [&](int slot, float (&m)[8], unsigned char (&c)[8]) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      m[e] = -INFINITY;
+      c[e] = 2;
+    }
+#pragma unroll
+    for (int dx = 0; dx < 5; ++dx) {
+      const uint4 u = srow[slot][(xl + dx) * 16 + c8];
+      const float4 lo = bf4_to_f4(make_uint2(u.x, u.y)), hi = bf4_to_f4(make_uint2(u.z, u.w));
+      const float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (v[e] > m[e]) {
+          m[e] = v[e];
+          c[e] = (unsigned char)dx;
+        }
+    }
+  };
+  float hm[5][8];
+  unsigned char hc[5][8];
+  fetch(y0 - 2);
+#pragma unroll
+  for (int r = 0; r < 5; ++r) {                     // rows y0-2 .. y0+1 into the window, y0+2 fetched
+    __syncthreads();
+    put(r & 1);
+    fetch(y0 - 1 + r);
+    __syncthreads();
+    if (r < 4) hmax(r & 1, hm[r], hc[r]);
+  }
+  // slot 0 holds row y0 + 2 (r = 4), pre holds row y0 + 3
+  int slot = 0;
+  for (int y = y0; y < y1; ++y) {
+    hmax(slot, hm[4], hc[4]);
+    __syncthreads();                                 // the slot about to be refilled has been read
+    slot ^= 1;
+    put(slot);                                       // row y + 3
+    fetch(y + 4);
+    float m[8];
+    unsigned char bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      m[e] = hm[0][e];
+      bi[e] = hc[0][e];
+#pragma unroll
+      for (int r = 1; r < 5; ++r)
+        if (hm[r][e] > m[e]) {
+          m[e] = hm[r][e];
+          bi[e] = (unsigned char)(5 * r) + hc[r][e];
+        }
+    }
+    const size_t o = (((size_t)b * H + y) * W + x0 + xl) * C + cg * 128 + c8 * 8;
+    *reinterpret_cast<uint4*>(out + o) =
+        make_uint4(pack_bf2(m[0], m[1]), pack_bf2(m[2], m[3]), pack_bf2(m[4], m[5]), pack_bf2(m[6], m[7]));
+    if (idx) {
+      uint2 kk;
+      kk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+      kk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+      *reinterpret_cast<uint2*>(idx + o) = kk;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        hm[r][e] = hm[r + 1][e];
+        hc[r][e] = hc[r + 1][e];
+      }
+    __syncthreads();                                 // the new slot is complete
+  }
+}
+
 // ---------------------------------------------------------------- host launchers
 hipError_t begin_conv(const float* x, const float* w, const float* bias, float* out, float* stats, int B, int H, int W,
-                      hipStream_t st, int mode) {
+                      hipStream_t st, int mode, bool h16) {
   if (W % BC_TP) return hipErrorInvalidValue;
   const int ntiles = B * H * (W / BC_TP);
+  if (h16) {   // bf16 output (training tape): bf16 mode, MFMA form
+    if (mode != MODE_BF16) return hipErrorInvalidValue;
+    const dim3 grid(std::min(ntiles, 256 * BM_WG_PER_CU));
+    hipLaunchKernelGGL((begin_conv_mfma_kernel<MODE_BF16, __bf16>), grid, dim3(256), 0, st, x, w, bias,
+                       reinterpret_cast<__bf16*>(out), stats, B, H, W);
+    return hipGetLastError();
+  }
   if (mode != MODE_F32 && !SDP_HEAD_DIRECT) {   // bf16 modes: the MFMA form
     const dim3 grid(std::min(ntiles, 256 * BM_WG_PER_CU));
     if (mode == MODE_F32X3)
@@ -964,8 +1083,14 @@ hipError_t begin_conv(const float* x, const float* w, const float* bias, float* 
 
 hipError_t end_conv(const float* in, const float* ss, const float* w, const float* bias, const float* sigmas,
                     const int64_t* labels, float* out, int B, int H, int W, int Cin, hipStream_t st,
-                    const LangevinArgs* lg, int mode) {
+                    const LangevinArgs* lg, int mode, bool h16) {
   if (Cin != EC_CIN) return hipErrorInvalidValue;
+  if (h16) {   // bf16 input (training tape): bf16 mode, scores only
+    if (mode != MODE_BF16 || lg || H % E2_TR || W % E2_TC) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((end_conv_mfma_kernel<MODE_BF16, false, __bf16>), dim3(B * (H / E2_TR) * (W / E2_TC)), dim3(256), 0, st,
+                       reinterpret_cast<const __bf16*>(in), ss, w, bias, sigmas, labels, out, H, W, LangevinArgs{});
+    return hipGetLastError();
+  }
   if (mode != MODE_F32 && !SDP_HEAD_DIRECT && H % E2_TR == 0 && W % E2_TC == 0) {   // bf16 modes: the MFMA form
     const dim3 grid(B * (H / E2_TR) * (W / E2_TC));
     const LangevinArgs la = lg ? *lg : LangevinArgs{};
@@ -1029,8 +1154,16 @@ hipError_t avgpool2(const float* in, float* out, int B, int H, int W, int C, hip
   return hipGetLastError();
 }
 
-hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx) {
+hipError_t maxpool5(const float* in, float* out, int B, int H, int W, int C, hipStream_t st, uint8_t* idx, bool h16) {
   if (C % 128 || W % MP_COLS) return hipErrorInvalidValue;
+  if (h16) {
+    if (W % MPH_COLS) return hipErrorInvalidValue;
+    auto hb = [&](int rows) { return B * ((H + rows - 1) / rows) * (W / MPH_COLS) * (C / 128); };
+    const int rows = hb(32) >= 1024 ? 32 : (hb(16) >= 1024 ? 16 : 8), grid = hb(rows);
+    hipLaunchKernelGGL(maxpool5_h16_kernel, dim3(grid), dim3(256), 0, st, reinterpret_cast<const __bf16*>(in),
+                       reinterpret_cast<__bf16*>(out), idx, B, H, W, C, rows);
+    return hipGetLastError();
+  }
   auto blocks = [&](int rows) { return B * ((H + rows - 1) / rows) * (W / MP_COLS) * (C / 128); };
   const int rows = blocks(32) >= MP_MIN_BLOCKS ? 32 : 16, grid = blocks(rows);
   if (idx)

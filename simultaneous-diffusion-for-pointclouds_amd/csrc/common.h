@@ -48,6 +48,25 @@ SDP_DEV void dma16_lds_opaque(i32x4 rsrc, uint32_t lds_byte, int voff, int soff)
                : "memory");   // m0 is reserved (not a clobber): nothing else in these kernels uses it
 }
 
+// ---- element access of activation tensors stored as float32 or, in the bf16 training tape
+// (train.hip), as bf16: 4 consecutive elements (i a multiple of 4) or one, always widened to float
+SDP_DEV float4 ldg4(const float* p, size_t i) { return *reinterpret_cast<const float4*>(p + i); }
+SDP_DEV float4 bf4_to_f4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+SDP_DEV float4 ldg4(const __bf16* p, size_t i) { return bf4_to_f4(*reinterpret_cast<const uint2*>(p + i)); }
+SDP_DEV uint32_t pack_bf2(float a, float b) {   // round-to-nearest-even, a in the low half
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+SDP_DEV uint2 f4_to_bf4(float4 v) { return make_uint2(pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)); }
+SDP_DEV void stg4(float* p, size_t i, float4 v) { *reinterpret_cast<float4*>(p + i) = v; }
+SDP_DEV void stg4(__bf16* p, size_t i, float4 v) { *reinterpret_cast<uint2*>(p + i) = f4_to_bf4(v); }
+SDP_DEV float ldg1(const float* p, size_t i) { return p[i]; }
+SDP_DEV float ldg1(const __bf16* p, size_t i) { return (float)p[i]; }
+
 SDP_DEV float elu(float x) { return x > 0.f ? x : (__expf(x) - 1.0f); }
 // the same values without a compare/select (e^x - 1 >= x, and e^min(x,0) - 1 = 0 for x > 0):
 // no VCC round trip, so it schedules freely between MFMAs
@@ -91,6 +110,9 @@ struct ConvArgs {
   const float* aux;
   const float* epi_ss;
   int dact;
+  // 1: every activation tensor of the launch (in, out, res, res2, out2, up, aux) holds bf16 elements
+  // (the bf16 training tape, train.hip; bf16 mode); the launchers pick the IO16 instantiation
+  int io16;
 };
 
 // Arguments of one weight-gradient launch (wgrad.hip).

@@ -96,6 +96,23 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (!a.circular && d != 1) { *why = "conv: zero padding only for d=1"; return hipErrorInvalidValue; }
   if (!a.pro_ss) { *why = "conv: prologue scale/shift table missing"; return hipErrorInvalidValue; }
   if (a.Cin > 1024 && a.ss_bstride == 0) { *why = "conv: identity table holds 1024 channels"; return hipErrorInvalidValue; }
+  if (a.io16) {   // the bf16 training tape: the shapes the training plan launches (conv_launch.h IO16)
+#ifndef SDP_CONV_BENCH_ONLY
+    if (mode != MODE_BF16) { *why = "conv: bf16 tensors (io16) need bf16 mode"; return hipErrorInvalidValue; }
+    const bool pe = a.pro_mode != PRO_NONE;
+    if (pool && ks == 1) return pe ? conv_launch<MODE_BF16, 1, 64, 1, true, true, true>(a, st)
+                                   : conv_launch<MODE_BF16, 1, 64, 1, true, false, true>(a, st);
+    if (pool) return pe ? conv_launch<MODE_BF16, 1, 64, 3, true, true, true>(a, st)
+                        : conv_launch<MODE_BF16, 1, 64, 3, true, false, true>(a, st);
+    // 16-wide tiles: 4-wave 128-Cout workgroups for both Cout widths (the 256-Cout layers as a pair per
+    // tile): with 8-channel staging units an 8-wave workgroup leaves 29 % of its units empty (720 for 1024
+    // slots) and ran the 256-class slower than the float32 tape (181 vs 168.5 us per B=8 launch)
+    if (ks == 3 && tc == 16)
+      return pe ? conv_launch_nj2<MODE_BF16, true, 4, true>(a, st) : conv_launch_nj2<MODE_BF16, false, 4, true>(a, st);
+#endif
+    *why = "conv: no bf16-tensor (io16) kernel for this shape";
+    return hipErrorInvalidValue;
+  }
   switch (mode) {
     case MODE_F32: return launch_mode<MODE_F32>(a, ks, pool, wm, tc, st);
     case MODE_F32X3: return launch_mode<MODE_F32X3>(a, ks, pool, wm, tc, st, half);

@@ -78,6 +78,16 @@ hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char**
   if (!a.pro_ss) { *why = "dgrad: prologue identity table missing"; return hipErrorInvalidValue; }
   if (!a.wf || a.wf16) { *why = "dgrad: weights in wf (the #dfrag packing), wf16 null"; return hipErrorInvalidValue; }
   const bool t16 = ks == 3 && a.circular && Ws % 16 == 0 && Hs % 8 == 0;
+  if (a.io16) {   // the bf16 training tape: the shapes the training plan launches (conv_launch.h IO16)
+#ifndef SDP_CONV_BENCH_ONLY
+    if (mode != MODE_BF16) { *why = "dgrad: bf16 tensors (io16) need bf16 mode"; return hipErrorInvalidValue; }
+    if (ks == 1) return dgrad_launch<MODE_BF16, 2, 32, 1, false, true>(a, st);
+    if (!a.circular) return dgrad_launch<MODE_BF16, 2, 32, 3, true, true>(a, st);
+    if (t16) return dgrad_launch_nj2<MODE_BF16, 4, true>(a, st);   // 128-Cout workgroups (see conv.hip's io16 forward)
+#endif
+    *why = "dgrad: no bf16-tensor (io16) kernel for this shape";
+    return hipErrorInvalidValue;
+  }
   switch (mode) {
     case MODE_F32X3: return launch_dgrad_mode<MODE_F32X3>(a, ks, wm, tc, t16, st);
     case MODE_BF16: return launch_dgrad_mode<MODE_BF16>(a, ks, wm, tc, t16, st);

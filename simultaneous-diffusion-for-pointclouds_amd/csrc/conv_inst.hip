@@ -30,15 +30,15 @@ namespace sdp {
 #define SDP_CONV_CPAIR 1
 #endif
 
-template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU>
+template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU, bool IO16>
 hipError_t conv_launch(ConvArgs a, hipStream_t st) {
-  using T = ConvTile<WM, TC, KS>;
+  using T = ConvTile<WM, TC, KS, 4, 4, IO16>;
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
   a.strip_w = conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / TC);
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   if constexpr (MODE != MODE_F32) {
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16, 4, (SDP_FWD_TRN && TC == 16 && !POOL)>),
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, POOL, POOL, PELU, 16, 4, (SDP_FWD_TRN && TC == 16 && !POOL), 4, IO16>),
                        grid, dim3(256), 0, st, a);
     return hipGetLastError();
   } else if constexpr (TC >= 32) {   // the 32x32 shape tiles rows in 32-pixel fragments
@@ -63,9 +63,9 @@ hipError_t conv_launch_half(ConvArgs a, hipStream_t st) {
 
 // 32-Cout waves, two per SIMD (conv_kernel.h ConvTile NJ = 2): 128 px x 128 Cout on 4 waves, two
 // workgroups per CU (pair), or 128 px x 256 Cout on 8 waves, one per CU (oct)
-template <int MODE, bool PELU, int NW>
+template <int MODE, bool PELU, int NW, bool IO16>
 hipError_t conv_launch_nj2(ConvArgs a, hipStream_t st) {
-  using T = ConvTile<1, 16, 3, NW, 2>;
+  using T = ConvTile<1, 16, 3, NW, 2, IO16>;
   a.tiles_per_img = a.H * a.W / (T::TR * 16);
   a.groups_per_img = a.H * a.W / 128;
   a.strip_w = NW == 8 ? conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / 16) : 0;
@@ -73,21 +73,21 @@ hipError_t conv_launch_nj2(ConvArgs a, hipStream_t st) {
   // of the XCD-ordered index, so a tile's second patch read comes from that XCD's L2
   a.cpair = (SDP_CONV_CPAIR && a.Cout == 2 * T::NTILE) ? 1 : 0;
   dim3 grid(a.B * a.tiles_per_img * (a.cpair ? 2 : 1), a.cpair ? 1 : a.Cout / T::NTILE);
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, NW, false, 2>), grid, dim3(T::NTH), 0,
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, NW, false, 2, IO16>), grid, dim3(T::NTH), 0,
                      st, a);
   return hipGetLastError();
 }
 
-template <int MODE, int WM, int TC, int KS, bool ZP>
+template <int MODE, int WM, int TC, int KS, bool ZP, bool IO16>
 hipError_t dgrad_launch(ConvArgs a, hipStream_t st) {
-  using T = ConvTile<WM, TC, KS>;
+  using T = ConvTile<WM, TC, KS, 4, 4, IO16>;
   a.tiles_per_img = a.H * a.W / (T::TR * TC);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
   if constexpr (TC < 32) {   // 8 x 16 tiles: the transposed direct epilogue (conv_kernel.h TRN)
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16, 4, true>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16, 4, true, 4, IO16>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16>), grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_mfma_kernel<MODE, WM, TC, KS, false, ZP, false, 16, 4, false, 4, IO16>), grid, dim3(256), 0, st, a);
   }
   return hipGetLastError();
 }
@@ -113,13 +113,13 @@ hipError_t dgrad_launch_half(ConvArgs a, hipStream_t st) {
 
 // data gradient on 32-Cout waves, two per SIMD (conv_kernel.h ConvTile NJ = 2, transposed epilogue):
 // 4 waves = 128 Cout per workgroup, two per CU; 8 waves = 256 Cout, one per CU
-template <int MODE, int NW>
+template <int MODE, int NW, bool IO16>
 hipError_t dgrad_launch_nj2(ConvArgs a, hipStream_t st) {
-  using T = ConvTile<1, 16, 3, NW, 2>;
+  using T = ConvTile<1, 16, 3, NW, 2, IO16>;
   a.tiles_per_img = a.H * a.W / (T::TR * 16);
   a.groups_per_img = a.H * a.W / 128;
   dim3 grid(a.B * a.tiles_per_img, a.Cout / T::NTILE);
-  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, false, 16, NW, true, 2>), grid, dim3(T::NTH), 0,
+  hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, false, 16, NW, true, 2, IO16>), grid, dim3(T::NTH), 0,
                      st, a);
   return hipGetLastError();
 }
@@ -132,7 +132,27 @@ template <> struct DgradShape<3> { static constexpr int WM = 1, TC = 64, KS = 3;
 template <> struct DgradShape<4> { static constexpr int WM = 1, TC = 32, KS = 3; static constexpr bool ZP = false; };
 template <> struct DgradShape<5> { static constexpr int WM = 1, TC = 16, KS = 3; static constexpr bool ZP = false; };  // 16x16 shape only
 
-#if defined(SDP_INST) && SDP_INST < 1000 && (SDP_INST % 10 == 6 || SDP_INST % 10 == 9)
+#if defined(SDP_INST) && SDP_INST >= 3000   // IO16 data gradients (bf16 tape): 0 = 1x1, 1 = zero-padded 3x3, 7 / 8 = 32-Cout waves on 4 / 8
+constexpr int kS = SDP_INST % 10;
+static_assert(kS == 0 || kS == 1 || kS == 7 || kS == 8, "SDP_INST: bad IO16 dgrad code");
+#if SDP_INST % 10 == 0
+template hipError_t dgrad_launch<MODE_BF16, 2, 32, 1, false, true>(ConvArgs, hipStream_t);
+#elif SDP_INST % 10 == 1
+template hipError_t dgrad_launch<MODE_BF16, 2, 32, 3, true, true>(ConvArgs, hipStream_t);
+#else
+template hipError_t dgrad_launch_nj2<MODE_BF16, kS == 7 ? 4 : 8, true>(ConvArgs, hipStream_t);
+#endif
+#elif defined(SDP_INST) && SDP_INST >= 2000   // IO16 forward (bf16 tape): 0 = pooled 1x1, 1 = pooled 3x3, 9 / 6 = nj2 on 4 / 8 waves
+constexpr int kPelu = (SDP_INST / 10) % 10, kS = SDP_INST % 10;
+static_assert(kPelu <= 1 && (kS == 0 || kS == 1 || kS == 6 || kS == 9), "SDP_INST: bad IO16 forward code");
+#if SDP_INST % 10 == 0
+template hipError_t conv_launch<MODE_BF16, 1, 64, 1, true, (kPelu != 0), true>(ConvArgs, hipStream_t);
+#elif SDP_INST % 10 == 1
+template hipError_t conv_launch<MODE_BF16, 1, 64, 3, true, (kPelu != 0), true>(ConvArgs, hipStream_t);
+#else
+template hipError_t conv_launch_nj2<MODE_BF16, (kPelu != 0), kS == 9 ? 4 : 8, true>(ConvArgs, hipStream_t);
+#endif
+#elif defined(SDP_INST) && SDP_INST < 1000 && (SDP_INST % 10 == 6 || SDP_INST % 10 == 9)
 constexpr int kMode = SDP_INST / 100 - 1, kPelu = (SDP_INST / 10) % 10;
 static_assert(kMode >= 1 && kMode <= 2 && kPelu <= 1, "SDP_INST: bad 32-Cout-wave forward code");
 template hipError_t conv_launch_nj2<kMode, (kPelu != 0), SDP_INST % 10 == 9 ? 4 : 8>(ConvArgs, hipStream_t);

@@ -65,7 +65,8 @@ constexpr int PSTRIDE = 144;  // bytes per staged patch pixel: 32 ch x (hi,lo bf
 // NJ = 16-Cout fragments per wave: 4 (128 px x 64 Cout per wave, one wave per SIMD, 512 registers), or
 // 2 (128 px x 32 Cout, two waves per SIMD at 256 registers: one wave's prologue, epilogue and waits run
 // under its partner's MFMAs) -- NW = 4 with two workgroups per CU (128 Cout), or NW = 8 (256 Cout).
-template <int WM, int TC, int KS, int NW = 4, int NJ = 4>
+// IO16: activations stored as bf16 (the training tape, train.hip): a 16-B staging unit holds 8 channels
+template <int WM, int TC, int KS, int NW = 4, int NJ = 4, bool IO16 = false>
 struct ConvTile {
   static constexpr int NTH = 64 * NW;              // threads per workgroup
   static constexpr int WN = NW / WM;               // waves along N
@@ -77,9 +78,10 @@ struct ConvTile {
   static constexpr int PC = TC + 2 * HALO;
   static constexpr int PR = TR + 2 * HALO;
   static constexpr int NPIX = PR * PC;
-  static constexpr int NU = (NPIX * 8 + NTH - 1) / NTH;        // 16-B staging units per thread per chunk
-  static constexpr int PATCH_BYTES = NU * (NTH / 8) * PSTRIDE;  // one transformed patch (+ slack: every
-                                                                //   staging unit has a pixel slot)
+  static constexpr int UPP = IO16 ? 4 : 8;                      // 16-B staging units per pixel and 32-channel chunk
+  static constexpr int NU = (NPIX * UPP + NTH - 1) / NTH;      // 16-B staging units per thread per chunk
+  static constexpr int PATCH_BYTES = NU * (NTH / UPP) * PSTRIDE;  // one transformed patch (+ slack: every
+                                                                  //   staging unit has a pixel slot)
   static constexpr int RAW_BYTES = NU * NTH * 16;               // raw fp32 patch landed by LDS-DMA
   static constexpr int PIPE_BYTES = 2 * PATCH_BYTES + RAW_BYTES;
   static constexpr int EPI_BYTES = WM * 64 * (NTILE + 8) * 4;   // LDS-staged epilogue (one half)
@@ -135,14 +137,22 @@ struct XformPlan {
 // D = W x X made the fp32x3 forward convs 2-3 % slower (256->256 165 -> 170 us, 128->128 @64x1024
 // 209 -> 213 us) while the bf16 training step ran 132.8 -> 137.0 image-steps/s with the transposed
 // direct epilogue on the data gradient (profiles/experiments/r03_trans_ab.log).
+// IO16 (the bf16 training tape, bf16 mode only): every activation tensor of the launch -- in, out, res, res2,
+// out2, up, aux -- holds bf16 elements: 16-B staging units of 8 channels (half the patch DMA bytes), bf16
+// epilogue loads and stores; statistics, bias and accumulation stay float32.
 template <int MODE, int WM, int TC, int KS, bool POOL, bool ZP, bool PELU, int SH = 32, int NW = 4, bool TRN = false,
-          int NJ = 4>
+          int NJ = 4, bool IO16 = false>
 __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)  // buffer-resource builtins exist only in the device pass
+  static_assert(!IO16 || MODE == MODE_BF16, "the bf16 tape runs in bf16 mode");
+  constexpr int ES = IO16 ? 2 : 4;                 // bytes per activation element
+  constexpr int CPU = IO16 ? 8 : 4;                // channels per 16-B staging unit
+  constexpr int USH = IO16 ? 2 : 3;                // log2(staging units per pixel-chunk)
+  constexpr int PPU = CPU / 2;                     // 2-channel transform pieces per unit
   static_assert((SH == 32) == (MODE == MODE_F32), "bf16 modes: 16x16 shape; exact fp32: 32x32");
   static_assert(NW == 4 || (SH == 16 && !POOL), "2-wave workgroups: the 16x16 non-pooled forward only");
   static_assert(NJ == 4 || (SH == 16 && !POOL && KS == 3 && WM == 1), "32-Cout waves: the 16x16 3x3 tiles only");
-  using T = ConvTile<WM, TC, KS, NW, NJ>;
+  using T = ConvTile<WM, TC, KS, NW, NJ, IO16>;
   constexpr int NTH = T::NTH;
   constexpr int NT = KS * KS;
   constexpr bool TRANS = TRN && SH == 16 && !POOL;
@@ -266,18 +276,17 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     }
   };
 
-  const float* inb = a.in + (size_t)b * a.H * a.W * Cin;
+  const char* inb = reinterpret_cast<const char*>(a.in) + (size_t)b * a.H * a.W * Cin * ES;
   // (scale, shift) rows of this image (the identity table when there is no affine prologue):
   // consumed only by the next chunk's transform, so the loads stay in flight across a chunk
   const float* ssb = a.pro_ss + (size_t)b * a.ss_bstride;
-  const int my_cv = tid & 7;                        // every unit of a thread has cv == tid % 8
-  // (scale, shift) of this thread's 4 channels, double-buffered by chunk parity: chunk c's rows live
-  // in ssv[c & 1][0..1] (the transform of chunk c writes patch buffer c & 1 too)
-  float4 ssv[2][2];
+  const int my_cv = tid & (T::UPP - 1);            // every unit of a thread has cv == tid % UPP
+  // (scale, shift) of this thread's CPU channels, double-buffered by chunk parity: chunk c's rows live
+  // in ssv[c & 1][..] (the transform of chunk c writes patch buffer c & 1 too); float4 k = channels 2k, 2k+1
+  float4 ssv[2][PPU];
   auto load_ss = [&](auto buf, int chunk) __attribute__((always_inline)) {
     constexpr int SB = decltype(buf)::value;
-    ssv[SB][0] = ld4(ssb + (chunk * 32 + my_cv * 4) * 2);
-    ssv[SB][1] = ld4(ssb + (chunk * 32 + my_cv * 4) * 2 + 4);
+    static_for<0, PPU>([&](auto kc) { ssv[SB][kc] = ld4(ssb + (chunk * 32 + my_cv * CPU) * 2 + 4 * decltype(kc)::value); });
   };
 
   // Staging unit u = 16 B (4 channels) of one patch pixel.  Its byte offset inside the image
@@ -288,15 +297,15 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   // num_records = the image's bytes: the (unconditional) DMA of a chunk past the last one
   // reads zeros instead of running off the tensor
   const __amdgpu_buffer_rsrc_t irs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, a.H * a.W * Cin * 4, 0x00020000);
+      __builtin_amdgcn_make_buffer_rsrc((void*)inb, 0, a.H * a.W * Cin * ES, 0x00020000);
   int uoff[NU];
   unsigned uvalid = 0;
   static_for<0, NU>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     int u = tid + k * NTH;
-    bool valid = u < T::NPIX * 8;
+    bool valid = u < T::NPIX * T::UPP;
     u = valid ? u : 0;
-    const int pix = u >> 3, cv = u & 7;
+    const int pix = u >> USH, cv = u & (T::UPP - 1);
     const int pr = pix / T::PC, pc = pix - pr * T::PC;
     int sr = sr0 - T::HALO + pr, sc = sc0 - T::HALO + pc;
     if (a.circular) {
@@ -308,7 +317,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       sc = min(max(sc, 0), Ws - 1);
     }
     const int y = sr * d + ph_r, x = sc * d + ph_c;
-    uoff[k] = ((y * a.W + x) * Cin + cv * 4) * 4;   // bytes, < 2^31 for every admitted shape
+    uoff[k] = ((y * a.W + x) * Cin + cv * CPU) * ES;   // bytes, < 2^31 for every admitted shape
     uvalid |= (valid ? 1u : 0u) << k;
   });
   // LDS-DMA of staging unit k: lane i of a wave lands 16 B at the wave-uniform base + 16*i
@@ -318,19 +327,19 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     const int base = __builtin_amdgcn_readfirstlane(((tid & ~63) + k * NTH) * 16);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
         irs, reinterpret_cast<__attribute__((address_space(3))) void*>(reinterpret_cast<uintptr_t>(raw + base)), 16,
-        uoff[k], chunk * 128, 0, SDP_DMA_AUX);
+        uoff[k], chunk * 32 * ES, 0, SDP_DMA_AUX);
   };
   // the same DMA as inline asm (common.h dma16_lds_opaque), for the main loop of the 3x3 tap schedule:
   // the compiler cannot tell the raw slots apart and would wait for every DMA in flight (vmcnt(0))
   // before the next raw read.  Ordering without that wait: unit k's slot is read again one chunk
   // later, and the weight loads issued after its DMA -- which complete in issue order with it --
   // are waited for two taps later, before their MFMAs
-  const i32x4 irs_o = buffer_desc(inb, (uint32_t)(a.H * a.W * Cin * 4));
+  const i32x4 irs_o = buffer_desc(inb, (uint32_t)(a.H * a.W * Cin * ES));
   auto load_unit_o = [&](auto kc, int chunk) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     if constexpr (SDP_KO & 1) return;
     const uint32_t base = (uint32_t)(uintptr_t)(raw + ((tid & ~63) + k * NTH) * 16);
-    dma16_lds_opaque(irs_o, base, uoff[k], chunk * 128);
+    dma16_lds_opaque(irs_o, base, uoff[k], chunk * 32 * ES);
   };
   // transform staging unit k of raw into patch buffer PB
   // transform of staging unit k: raw (fp32, landed by this thread's own DMA) -> patch buffer PB
@@ -341,7 +350,24 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   auto xform_store = [&](auto kc, auto pb, float4 v) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value;
     constexpr int PB = decltype(pb)::value;
-    const int pix = (tid + k * NTH) >> 3;   // units past the patch land in its slack: no branch
+    const int pix = (tid + k * NTH) >> USH;   // units past the patch land in its slack: no branch
+    if constexpr (IO16) {   // 8 bf16 channels -> prologue -> 8 bf16 (one 16-B LDS write)
+      const uint4 u = __builtin_bit_cast(uint4, v);
+      const float4 lo = bf4_to_f4(make_uint2(u.x, u.y)), hi = bf4_to_f4(make_uint2(u.z, u.w));
+      float x8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float4 sv = ssv[PB][e >> 1];
+        x8[e] = fmaf(x8[e], (e & 1) ? sv.z : sv.x, (e & 1) ? sv.w : sv.y);
+        if constexpr (PELU) x8[e] = elu_max(x8[e]);
+        if constexpr (ZP) {
+          if (!((uvalid >> k) & 1u)) x8[e] = 0.f;
+        }
+      }
+      *reinterpret_cast<uint4*>(lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 16) =
+          make_uint4(pack_bf2(x8[0], x8[1]), pack_bf2(x8[2], x8[3]), pack_bf2(x8[4], x8[5]), pack_bf2(x8[6], x8[7]));
+      return;
+    }
     const float4 ssv0 = ssv[PB][0], ssv1 = ssv[PB][1];
     v.x = fmaf(v.x, ssv0.x, ssv0.y);
     v.y = fmaf(v.y, ssv0.z, ssv0.w);
@@ -375,8 +401,16 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   auto xform_piece = [&](auto kc, auto hc, auto pb, float4 v4) __attribute__((always_inline)) {
     constexpr int k = decltype(kc)::value, h = decltype(hc)::value, PB = decltype(pb)::value;
     if constexpr (SDP_KO & 2) return;
-    const int pix = (tid + k * NTH) >> 3;
-    float x0 = h ? v4.z : v4.x, x1 = h ? v4.w : v4.y;
+    const int pix = (tid + k * NTH) >> USH;
+    float x0, x1;
+    if constexpr (IO16) {   // piece h = channels 2h, 2h+1 = the two bf16 halves of word h
+      const uint32_t w = __float_as_uint(h == 0 ? v4.x : h == 1 ? v4.y : h == 2 ? v4.z : v4.w);
+      x0 = __uint_as_float(w << 16);
+      x1 = __uint_as_float(w & 0xffff0000u);
+    } else {
+      x0 = h ? v4.z : v4.x;
+      x1 = h ? v4.w : v4.y;
+    }
     const float4 sv = ssv[PB][h];
     x0 = fmaf(x0, sv.x, sv.y);
     x1 = fmaf(x1, sv.z, sv.w);
@@ -393,7 +427,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     bf16x2 hi;
     hi[0] = (__bf16)x0;
     hi[1] = (__bf16)x1;
-    char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 8 + h * 4;
+    char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * (2 * CPU) + h * 4;
     *reinterpret_cast<bf16x2*>(dst) = hi;
     if constexpr (MODE == MODE_F32X3) {
       bf16x2 lo;
@@ -543,9 +577,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
               acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc4[mb][nj], 0, 0, 0);
             }
           }
-          if constexpr (blk < 2 * NX) xform_piece(std::integral_constant<int, tap + XT * (blk >> 1)>{},
-                                                  std::integral_constant<int, blk & 1>{},
-                                                  std::integral_constant<int, 1 - P>{}, xv[blk >> 1]);
+          if constexpr (blk < PPU * NX) xform_piece(std::integral_constant<int, tap + XT * (blk / PPU)>{},
+                                                    std::integral_constant<int, blk % PPU>{},
+                                                    std::integral_constant<int, 1 - P>{}, xv[blk / PPU]);
           __builtin_amdgcn_sched_barrier(0);
         });
         if constexpr (NT == 1) dmas();
@@ -570,7 +604,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   //   blocks 0, 1            : the raw values of the units this tap transforms (XformPlan::tap_of)
   //   blocks 2 .. 31         : their transform, 5 stages per 2-channel piece
   //   blocks 30, 31          : the LDS-DMA of those units for the chunk after next (raw slot free)
-  using XP = XformPlan<NU, NT, MODE == MODE_BF16 ? 8 : 5>;
+  using XP = XformPlan<NU, NT, (MODE == MODE_BF16 && !IO16) ? 8 : 5>;   // (IO16: 4 pieces per unit)
   constexpr int NQ = MODE == MODE_F32X3 ? 8 : 4;   // A reads per half tap
   constexpr int NWL = NJ * (MODE == MODE_F32X3 ? 2 : 1);   // weight loads per tap
   constexpr int NBLK = 8 * NJ;                     // MFMA blocks per tap: (half s, Cout fragment nj, px group i)
@@ -606,19 +640,31 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     static_for<0, NT>([&](auto tap_c) {
       constexpr int tap = decltype(tap_c)::value;
       constexpr int CUR = tap % 3, NXT = (tap + 2) % 3;
-      constexpr int U0 = XP::first(tap), UN = XP::count(tap), Q = UN * 2 * XP::NSTG;
+      constexpr int U0 = XP::first(tap), UN = XP::count(tap), Q = UN * PPU * XP::NSTG;
       constexpr int UNA = UN > 0 ? UN : 1;
       const int wchunk = tap + 2 < NT ? chunk : min(chunk + 1, nchunks - 1);
       constexpr int wtap = tap + 2 < NT ? tap + 2 : tap + 2 - NT;
       float4 xr[UNA];                                  // raw values of this tap's units
-      float py0[2 * UNA], py1[2 * UNA], pe0[2 * UNA], pe1[2 * UNA];
-      uint32_t phi[2 * UNA], plo[2 * UNA];
+      float py0[PPU * UNA], py1[PPU * UNA], pe0[PPU * UNA], pe1[PPU * UNA];
+      uint32_t phi[PPU * UNA], plo[PPU * UNA];
       // stage st of piece pc (unit U0 + pc / 2, channels 2 (pc % 2) ..): the xform_piece arithmetic,
       // split so that each stage fits one block's free issue cycles
       auto stage = [&](auto pc_c, auto st_c) __attribute__((always_inline)) {
         constexpr int pc = decltype(pc_c)::value, st = decltype(st_c)::value;
-        constexpr int j = pc / 2, h = pc % 2, k = U0 + j, PB = 1 - P;
+        constexpr int j = pc / PPU, h = pc % PPU, k = U0 + j, PB = 1 - P;
         if constexpr (SDP_KO & 2) return;
+        // the piece's two raw values (IO16: the bf16 halves of word h of the unit)
+        auto raw2 = [&](float& r0, float& r1) __attribute__((always_inline)) {
+          const float4 v = xr[j];
+          if constexpr (IO16) {
+            const uint32_t w = __float_as_uint(h == 0 ? v.x : h == 1 ? v.y : h == 2 ? v.z : v.w);
+            r0 = __uint_as_float(w << 16);
+            r1 = __uint_as_float(w & 0xffff0000u);
+          } else {
+            r0 = h ? v.z : v.x;
+            r1 = h ? v.w : v.y;
+          }
+        };
         if constexpr (XP::NSTG == 8) {   // bf16: the same arithmetic one value at a time
           const float4 v = xr[j];
           const float4 sv = ssv[PB][h];
@@ -651,10 +697,11 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
           return;
         }
         if constexpr (st == 0) {
-          const float4 v = xr[j];
+          float r0, r1;
+          raw2(r0, r1);
           const float4 sv = ssv[PB][h];
-          py0[pc] = fmaf(h ? v.z : v.x, sv.x, sv.y);
-          py1[pc] = fmaf(h ? v.w : v.y, sv.z, sv.w);
+          py0[pc] = fmaf(r0, sv.x, sv.y);
+          py1[pc] = fmaf(r1, sv.z, sv.w);
           if constexpr (PELU) {
             pe0[pc] = fminf(py0[pc], 0.f);
             pe1[pc] = fminf(py1[pc], 0.f);
@@ -687,8 +734,8 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
             plo[pc] = *reinterpret_cast<const uint32_t*>(&lo);
           }
         } else {
-          const int pix = (tid + k * NTH) >> 3;
-          char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 8 + h * 4;
+          const int pix = (tid + k * NTH) >> USH;
+          char* dst = lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * (2 * CPU) + h * 4;
           *reinterpret_cast<uint32_t*>(dst) = phi[pc];
           if constexpr (MODE == MODE_F32X3) *reinterpret_cast<uint32_t*>(dst + 64) = plo[pc];
         }
@@ -750,7 +797,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   // (the data-gradient launches keep do_chunk: in bf16 training the tap schedule measured 3-5 % slower
   // on them, profiles/experiments/r05_train_kernel_stats_ab.log)
   if constexpr (MODE != MODE_F32 && NT == 9 && !TRANS) {
-    static_assert(XP::max_count() * 2 * XP::NSTG <= 2 * (NBLK - 2), "at most two transform stages per block");
+    static_assert(XP::max_count() * PPU * XP::NSTG <= 2 * (NBLK - 2), "at most two transform stages per block");
     for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
       do_chunk9(std::integral_constant<int, 0>{}, chunk);
       do_chunk9(std::integral_constant<int, 1>{}, chunk + 1);
@@ -777,24 +824,38 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
     const int Ho = a.H, Wo = a.W;
     const size_t bo = (size_t)b * Ho * Wo * Cout;
-    const int img_bytes = Ho * Wo * Cout * 4;
-    auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p + bo), 0, img_bytes, 0x00020000); };
+    const int img_bytes = Ho * Wo * Cout * ES;
+    auto rs = [&](const float* p) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(reinterpret_cast<const char*>(p) + bo * ES), 0, img_bytes, 0x00020000);
+    };
     const int lq = lane >> 4, lcol = lane & 15;
     constexpr int CB = TC / 16;                      // 16-px fragments per tile row
-    const int voff = (lcol * d * Cout + 4 * lq) * 4; // lane part of every byte offset
+    const int voff = (lcol * d * Cout + 4 * lq) * ES; // lane part of every byte offset
     auto soff = [&](int mb, int nj) {                // wave-uniform part: fragment mb's first pixel, channel block nj
       const int mr = mb / CB, mc = (mb % CB) * 16;
       const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc) * d + ph_c;
-      return __builtin_amdgcn_readfirstlane(((y * Wo + x) * Cout + n0 + wn * 16 * NJ + nj * 16) * 4);
+      return __builtin_amdgcn_readfirstlane(((y * Wo + x) * Cout + n0 + wn * 16 * NJ + nj * 16) * ES);
     };
     auto ld = [&](__amdgpu_buffer_rsrc_t r, int so) {
-      const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, voff, so, 0);
-      return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
+      if constexpr (IO16) {   // 4 bf16 channels: 8 B per lane
+        typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+        const u32x2 q = __builtin_amdgcn_raw_buffer_load_b64(r, voff, so, 0);
+        return bf4_to_f4(make_uint2(q.x, q.y));
+      } else {
+        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(r, voff, so, 0);
+        return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
+      }
     };
     auto st = [&](float4 v, __amdgpu_buffer_rsrc_t r, int so, auto aux_c) {
       constexpr int AUX = decltype(aux_c)::value;
-      const u32x4 q = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
-      __builtin_amdgcn_raw_buffer_store_b128(q, r, voff, so, AUX);
+      if constexpr (IO16) {
+        typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+        const uint2 w = f4_to_bf4(v);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{w.x, w.y}, r, voff, so, AUX);
+      } else {
+        const u32x4 q = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+        __builtin_amdgcn_raw_buffer_store_b128(q, r, voff, so, AUX);
+      }
     };
     auto rs_or_out = [&](const float* p) { return rs(p ? p : a.out); };
     const __amdgpu_buffer_rsrc_t ors = rs(a.out), xrs = rs_or_out(a.aux), rrs = rs_or_out(a.res), o2rs = rs_or_out(a.out2),
@@ -825,7 +886,8 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor
         const int Hi = a.H / 2, Wi = a.W / 2;
         const float shh = (float)(Hi - 1) / (float)(a.H - 1), sww = (float)(Wi - 1) / (float)(a.W - 1);
-        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co0;
+        const size_t ub = (size_t)b * Hi * Wi * Cout + co0;
+        auto lup = [&](size_t e) { return IO16 ? ldg4(reinterpret_cast<const __bf16*>(a.up), e) : ldg4(a.up, e); };
 #pragma unroll
         for (int mb = 0; mb < 8; ++mb) {
           const int mr = mb / CB, mc = (mb % CB) * 16;
@@ -834,9 +896,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
           const int y0 = (int)fy, x0 = (int)fx;
           const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
           const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
-          const float4 v00 = ld4(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = ld4(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
-          const float4 v10 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
-          const float4 v11 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
+          const float4 v00 = lup(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = lup(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
+          const float4 v10 = lup(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
+          const float4 v11 = lup(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
           auto bil = [&](float a00, float a01, float a10, float a11) {
             return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
           };
@@ -934,15 +996,18 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     __builtin_amdgcn_s_waitcnt(0);   // the last (dead) DMA may still be landing in raw
     const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
     const size_t bo = (size_t)b * Ho * Wo * Cout;
-    const int img_bytes = Ho * Wo * Cout * 4;
-    auto rs = [&](const float* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)(p ? p + bo : a.out + bo), 0, img_bytes, 0x00020000); };
+    const int img_bytes = Ho * Wo * Cout * ES;
+    auto rs = [&](const float* p) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(reinterpret_cast<const char*>(p ? p : a.out) + bo * ES), 0, img_bytes,
+                                               0x00020000);
+    };
     const __amdgpu_buffer_rsrc_t ors = rs(a.out), rrs = rs(a.res), o2rs = rs(a.out2), r2rs = rs(a.res2), xrs = rs(a.aux);
     const int lq = lane >> 4, lcol = lane & 15;
     constexpr int CB = TC / 16;                      // 16-px fragments per tile row
     constexpr int NF = POOL ? CB : 8;                // fragments (pooled: row-0 fragments) per lane
     constexpr int PER = POOL ? 2 : 4;                // values per fragment and lane
     constexpr int NV = NF * PER;
-    const int xs = (POOL ? 1 : d) * Cout * 4;        // bytes between consecutive output pixels of a run
+    const int xs = (POOL ? 1 : d) * Cout * ES;       // bytes between consecutive output pixels of a run
     // byte offset of value i of channel block nj: a per-fragment VGPR base (channel block 0) and a
     // wave-uniform SGPR part (the value's pixel step, the block's 64-B channel offset)
     int vbase[NF];
@@ -950,14 +1015,44 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       constexpr int f = decltype(fc)::value;
       const int co = n0 + wn * 16 * NJ + lcol;
       if constexpr (POOL) {
-        vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 16) >> 1) + 2 * lq) * Cout + co) * 4;
+        vbase[f] = (((sr0 >> 1) * Wo + ((sc0 + f * 16) >> 1) + 2 * lq) * Cout + co) * ES;
       } else {
         constexpr int mr = f / CB, mc = (f % CB) * 16;
         const int y = (sr0 + wrow0 + mr) * d + ph_r, x = (sc0 + mc + 4 * lq) * d + ph_c;
-        vbase[f] = ((y * Wo + x) * Cout + co) * 4;
+        vbase[f] = ((y * Wo + x) * Cout + co) * ES;
       }
     });
-#define SDP_EPI16_OFF(i, nj) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs + (nj) * 64)
+#define SDP_EPI16_OFF(i, nj) vbase[(i) / PER], __builtin_amdgcn_readfirstlane(((i) % PER) * xs + (nj) * 16 * ES)
+    // one value of a tensor (IO16: a bf16 element, widened)
+    auto ld1 = [&](__amdgpu_buffer_rsrc_t r, int vo, int so) __attribute__((always_inline)) {
+      if constexpr (IO16) return __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0) << 16);
+      else return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+    };
+    // the NV values of channel block nj: float per value, or (IO16) bf16 pairs of adjacent channels --
+    // lanes l and l ^ 1 hold channels c, c ^ 1 of the same pixels: each swaps half its values with its
+    // partner (DPP quad_perm [1,0,3,2]) so that a lane stores 4 B = both channels of PER / 2 pixels
+    auto store_vals = [&](const float (&w)[NV], __amdgpu_buffer_rsrc_t r, auto nj_c, auto aux_c) __attribute__((always_inline)) {
+      constexpr int NJC = decltype(nj_c)::value, AUX = decltype(aux_c)::value;
+      if constexpr (IO16) {
+        constexpr int HP = PER / 2;
+        const bool odd = lane & 1;
+#pragma unroll
+        for (int f = 0; f < NF; ++f) {
+          const int vb = vbase[f] + (odd ? HP * xs - 2 : 0);
+#pragma unroll
+          for (int k = 0; k < HP; ++k) {
+            const float mine = odd ? w[f * PER + HP + k] : w[f * PER + k];
+            const float send = odd ? w[f * PER + k] : w[f * PER + HP + k];
+            const float got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0xB1, 0xf, 0xf, false));
+            const uint32_t pk = odd ? pack_bf2(got, mine) : pack_bf2(mine, got);
+            __builtin_amdgcn_raw_buffer_store_b32(pk, r, vb, __builtin_amdgcn_readfirstlane(k * xs + NJC * 16 * ES), AUX);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(w[i]), r, SDP_EPI16_OFF(i, NJC), AUX);
+      }
+    };
     // The bias and the addend of every channel block (the residual, else the CRP second output's res2)
     // are loaded before the first store: loads and stores retire through one in-order counter on gfx9,
     // so a block's loads issued after the previous block's stores would wait for their acknowledgement
@@ -968,8 +1063,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       const __amdgpu_buffer_rsrc_t prs = a.res ? rrs : r2rs;
       static_for<0, NJ>([&](auto njc) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i)
-          pre[njc][i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(prs, SDP_EPI16_OFF(i, decltype(njc)::value), 0));
+        for (int i = 0; i < NV; ++i) pre[njc][i] = ld1(prs, SDP_EPI16_OFF(i, decltype(njc)::value));
       });
     }
     static_for<0, NJ>([&](auto njc) {
@@ -997,7 +1091,8 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       if (a.up) {   // F.interpolate(bilinear, align_corners=True) of a [H/2][W/2] tensor (non-pooled)
         const int Hi = a.H / 2, Wi = a.W / 2;
         const float shh = (float)(Hi - 1) / (float)(a.H - 1), sww = (float)(Wi - 1) / (float)(a.W - 1);
-        const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co;
+        const size_t ub = (size_t)b * Hi * Wi * Cout + co;
+        auto lu = [&](size_t e) { return IO16 ? ldg1(reinterpret_cast<const __bf16*>(a.up), e) : ldg1(a.up, e); };
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
           const int f = i / PER, k = i % PER;
@@ -1007,9 +1102,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
           const int y0 = (int)fy, x0 = (int)fx;
           const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
           const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
-          const float v00 = ub[((size_t)y0 * Wi + x0) * Cout], v01 = ub[((size_t)y0 * Wi + x0 + xp) * Cout];
-          const float v10 = ub[((size_t)(y0 + yp) * Wi + x0) * Cout];
-          const float v11 = ub[((size_t)(y0 + yp) * Wi + x0 + xp) * Cout];
+          const float v00 = lu(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = lu(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
+          const float v10 = lu(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
+          const float v11 = lu(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
           v[i] = v[i] + (ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11));
         }
       }
@@ -1021,7 +1116,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
         }
 #pragma unroll
         for (int i = 0; i < NV; ++i) {
-          float h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, SDP_EPI16_OFF(i, nj), 0));
+          float h = ld1(xrs, SDP_EPI16_OFF(i, nj));
           if (a.dact == 3) h = fmaf(h, esc, esh);
           v[i] = v[i] * elu_grad(h, a.dact);
         }
@@ -1034,18 +1129,16 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
         float r2[NV];
 #pragma unroll
         for (int i = 0; i < NV; ++i)   // (a residual and a second output together: loaded here, all before the stores)
-          r2[i] = a.res ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r2rs, SDP_EPI16_OFF(i, nj), 0)) : pre[nj][i];
+          r2[i] = a.res ? ld1(r2rs, SDP_EPI16_OFF(i, nj)) : pre[nj][i];
 #pragma unroll
-        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i] + r2[i]), o2rs, SDP_EPI16_OFF(i, nj), 0);
+        for (int i = 0; i < NV; ++i) r2[i] = v[i] + r2[i];
+        store_vals(r2, o2rs, njc, std::integral_constant<int, 0>{});
       }
       if (a.epi_elu) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] = elu(v[i]);
       }
-      if constexpr (!(SDP_KO & 16)) {
-#pragma unroll
-        for (int i = 0; i < NV; ++i) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[i]), ors, SDP_EPI16_OFF(i, nj), SDP_STORE_AUX);
-      }
+      if constexpr (!(SDP_KO & 16)) store_vals(v, ors, njc, std::integral_constant<int, SDP_STORE_AUX>{});
       if (a.stats) {
         float sum = 0.f;
 #pragma unroll
@@ -1103,7 +1196,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       es1 = ld4(a.epi_ss + ((size_t)b * Cout + co0) * 2 + 4);
     }
     const int Ho = POOL ? a.H / 2 : a.H, Wo = POOL ? a.W / 2 : a.W;
-    float* outb = a.out + (size_t)b * Ho * Wo * Cout;
+    using TA = std::conditional_t<IO16, __bf16, float>;   // activation element type
+    auto tp = [](const float* p) { return reinterpret_cast<const TA*>(p); };
+    TA* const outb = reinterpret_cast<TA*>(a.out) + (size_t)b * Ho * Wo * Cout;
     // shifted sums per (stats group, channel): K = the thread's first value
     float4 sK[WM], s1[WM], s2[WM];
     int sn[WM];
@@ -1165,9 +1260,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
         int y, x, g;
         pix(min(j, NPO - 1), y, x, g);
         const size_t oi = bo + ((size_t)y * Wo + x) * Cout + co0;
-        o.h = a.aux ? ld4(a.aux + oi) : make_float4(0.f, 0.f, 0.f, 0.f);
-        o.r = a.res ? ld4(a.res + oi) : make_float4(0.f, 0.f, 0.f, 0.f);
-        o.q = a.out2 ? ld4(a.res2 + oi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        o.h = a.aux ? ldg4(tp(a.aux), oi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        o.r = a.res ? ldg4(tp(a.res), oi) : make_float4(0.f, 0.f, 0.f, 0.f);
+        o.q = a.out2 ? ldg4(tp(a.res2), oi) : make_float4(0.f, 0.f, 0.f, 0.f);
         return o;
       };
       Ops nx = fetch(pl);
@@ -1200,10 +1295,10 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
           const int y0 = (int)fy, x0 = (int)fx;
           const int yp = y0 < Hi - 1 ? 1 : 0, xp = x0 < Wi - 1 ? 1 : 0;
           const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
-          const float* ub = a.up + (size_t)b * Hi * Wi * Cout + co0;
-          const float4 v00 = ld4(ub + ((size_t)y0 * Wi + x0) * Cout), v01 = ld4(ub + ((size_t)y0 * Wi + x0 + xp) * Cout);
-          const float4 v10 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0) * Cout);
-          const float4 v11 = ld4(ub + ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
+          const TA* ub = tp(a.up) + (size_t)b * Hi * Wi * Cout + co0;
+          const float4 v00 = ldg4(ub, ((size_t)y0 * Wi + x0) * Cout), v01 = ldg4(ub, ((size_t)y0 * Wi + x0 + xp) * Cout);
+          const float4 v10 = ldg4(ub, ((size_t)(y0 + yp) * Wi + x0) * Cout);
+          const float4 v11 = ldg4(ub, ((size_t)(y0 + yp) * Wi + x0 + xp) * Cout);
           auto bil = [&](float a00, float a01, float a10, float a11) {
             return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
           };
@@ -1226,9 +1321,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
         }
         if (a.res) v = make_float4(cu.r.x + v.x, cu.r.y + v.y, cu.r.z + v.z, cu.r.w + v.w);
         if (a.out2)
-          *reinterpret_cast<float4*>(a.out2 + bo + oidx) = make_float4(v.x + cu.q.x, v.y + cu.q.y, v.z + cu.q.z, v.w + cu.q.w);
+          stg4(reinterpret_cast<TA*>(a.out2), bo + oidx, make_float4(v.x + cu.q.x, v.y + cu.q.y, v.z + cu.q.z, v.w + cu.q.w));
         if (a.epi_elu) v = make_float4(elu(v.x), elu(v.y), elu(v.z), elu(v.w));
-        if constexpr (!(SDP_KO & 16)) *reinterpret_cast<float4*>(outb + oidx) = v;
+        if constexpr (!(SDP_KO & 16)) stg4(outb, oidx, v);
         static_for<0, WM>([&](auto gc) {
           constexpr int gg = decltype(gc)::value;
           if (gg == g) {

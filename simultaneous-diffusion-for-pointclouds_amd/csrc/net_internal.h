@@ -56,6 +56,7 @@ struct sdp_net {
   bool arena_owned = false;         // false once the caller bound its own arena
   bool finalized = false;
   bool train_packs = false;         // keep the dgrad packings current in repack()
+  bool tape16 = true;               // bf16 mode: the training tape in bf16 (sdp_net_set_tape)
   int mode = sdp::MODE_F32X3;
   sdp::TrainPlan* plan = nullptr;   // tape of the last sdp_net_forward_train
   int split = 0;                     // part-batch forwards (0: the default, 2)

@@ -24,6 +24,8 @@
 
 namespace sdp {
 
+// an NHWC activation / gradient tensor of the tape: float32, or bf16 elements when the plan's h16 is set
+// (p is then reinterpreted by the kernels: every launch below passes h16 along)
 struct T4 {
   float* p;
   int H, W, C;
@@ -34,6 +36,11 @@ struct TrainPlan {
   int B = 0, H = 0, W = 0, C = 0;
   hipStream_t st = nullptr;
   bool dry = true;
+  // the bf16 tape (bf16 mode, sdp_net_set_tape): every activation and output gradient is stored once in
+  // bf16 -- half the bytes of every conv's patch DMA and epilogue, of the weight gradient's two operand
+  // streams and of the memory-bound adjoints; parameters, the gradient arena, statistics and the head's
+  // scores stay float32
+  bool h16 = false;
   char* base = nullptr;
   size_t cap = 0, used = 0;
   std::map<std::string, T4> saved;
@@ -61,14 +68,15 @@ struct TrainPlan {
   size_t ws_need = 0;                 // forward + backward bytes (dry run), 0 = unknown
 
   // ------------------------------------------------------------------ allocation
-  float* take(size_t nfloats) {
-    const size_t bytes = (nfloats * 4 + 255) / 256 * 256;
+  float* takeb(size_t nbytes) {
+    const size_t bytes = (nbytes + 255) / 256 * 256;
     float* p = dry ? nullptr : reinterpret_cast<float*>(base + used);
     used += bytes;
     if (!dry && used > cap) throw std::runtime_error("training workspace too small");
     return p;
   }
-  T4 mk(int h, int w, int c) { return T4{take((size_t)B * h * w * c), h, w, c}; }
+  float* take(size_t nfloats) { return takeb(nfloats * 4); }
+  T4 mk(int h, int w, int c) { return T4{takeb((size_t)B * h * w * c * (h16 ? 2 : 4)), h, w, c}; }
   T4 like(const T4& t) { return mk(t.H, t.W, t.C); }
   size_t n(const T4& t) const { return (size_t)B * t.H * t.W * t.C; }
   void ok(hipError_t e, const std::string& what) {
@@ -148,6 +156,7 @@ struct TrainPlan {
     a.circular = o.circular ? 1 : 0;
     a.pro_mode = o.pro;
     a.epi_elu = o.epi_elu ? 1 : 0;
+    a.io16 = h16 ? 1 : 0;
     const char* why = "conv launch";
     ok(conv_mfma(net->mode, a, (int)hp.shape[2], o.pool, st, &why), std::string(why) + " (" + wkey + ")");
   }
@@ -241,13 +250,13 @@ struct TrainPlan {
     uint8_t* i2 = reinterpret_cast<uint8_t*>(take(nidx));
     idxs[k + ".i1"] = i1;
     idxs[k + ".i2"] = i2;
-    if (!dry) ok(maxpool5(X.p, p1.p, B, X.H, X.W, X.C, st, i1), "maxpool5");
+    if (!dry) ok(maxpool5(X.p, p1.p, B, X.H, X.W, X.C, st, i1, h16), "maxpool5");
     Opt a;
     a.bias = false;
     a.out2 = x1.p;
     a.res2 = X.p;
     conv(p1, k + ".convs.0", path1, a);
-    if (!dry) ok(maxpool5(path1.p, p2.p, B, X.H, X.W, X.C, st, i2), "maxpool5");
+    if (!dry) ok(maxpool5(path1.p, p2.p, B, X.H, X.W, X.C, st, i2, h16), "maxpool5");
     Opt b;
     b.bias = false;
     b.res = x1.p;
@@ -303,7 +312,8 @@ struct TrainPlan {
     mvs = take((size_t)B * 2 * C * 4);
     T4 x0 = mk(H, W, C);
     if (!dry)
-      ok(begin_conv(xin, P("begin_conv.weight"), P("begin_conv.bias"), x0.p, stats, B, H, W, st, net->mode), "begin_conv");
+      ok(begin_conv(xin, P("begin_conv.weight"), P("begin_conv.bias"), x0.p, stats, B, H, W, st, net->mode, h16),
+         "begin_conv");
     T4 l1 = resf("res1.0", x0, false, 1, H * W / 64, 64.f);
     l1 = resf("res1.1", l1, false, 1, tiles(l1), 128.f);
     T4 l2 = resf("res2.0", l1, true, 1, tiles(l1), 128.f);
@@ -319,7 +329,7 @@ struct TrainPlan {
     norm("normalizer", tiles(o), 128.f, C);
     if (!dry)
       ok(end_conv(o.p, F("normalizer#ss"), P("end_conv.weight"), P("end_conv.bias"), P("sigmas"), lab, out, B, H, W, C,
-                  st, nullptr, net->mode),
+                  st, nullptr, net->mode, h16),
          "end_conv");
     fwd_bytes = used;
   }
@@ -350,7 +360,7 @@ struct TrainPlan {
     a.dil = dil;
     a.circular = circular ? 1 : 0;
     const char* why = "wgrad launch";
-    ok(conv_wgrad(net->mode, a, ks, G(k + ".weight"), with_bias ? G(k + ".bias") : nullptr, 0, st, &why),
+    ok(conv_wgrad(net->mode, a, ks, G(k + ".weight"), with_bias ? G(k + ".bias") : nullptr, 0, st, &why, h16),
        std::string(why) + " (" + k + ")");
   }
   void dgrad(const std::string& k, const T4& dy, const T4& dx, int dil, bool circular, int ks, int dact,
@@ -373,13 +383,14 @@ struct TrainPlan {
     a.aux = aux;
     a.epi_ss = epi_ss;
     a.dact = dact;
+    a.io16 = h16 ? 1 : 0;
     const char* why = "dgrad launch";
     ok(conv_dgrad(net->mode, a, ks, st, &why), std::string(why) + " (" + k + ")");
   }
   void inpp_back(const std::string& nkey, const T4& g, const T4& h, const float* r1, const float* r2, const T4& out) {
     if (!dry)
       ok(inpp_backward(g.p, h.p, F(nkey + "#nst"), P(nkey + ".alpha"), P(nkey + ".gamma"), B, h.H * h.W, h.C, spart,
-                       coef, ppart, G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st),
+                       coef, ppart, G(nkey + ".alpha"), G(nkey + ".gamma"), G(nkey + ".beta"), r1, r2, out.p, st, h16),
          "inpp_backward " + nkey);
     finished({nkey + ".alpha", nkey + ".gamma", nkey + ".beta"});
   }
@@ -391,7 +402,7 @@ struct TrainPlan {
     const float* sg;
     if (down && dil == 1) {
       T4 dyf = mk(x.H, x.W, dout.C);
-      if (!dry) ok(unpool(dout.p, dyf.p, B, x.H, x.W, dout.C, st), "unpool");
+      if (!dry) ok(unpool(dout.p, dyf.p, B, x.H, x.W, dout.C, st, h16), "unpool");
       wgrad(k + ".conv2.conv", h1, PRO_AFFINE_ELU, ss2, dyf, 1, false, 3, true);
       dgrad(k + ".conv2.conv", dyf, g2, 1, false, 3, 3, h1.p, ss2, nullptr);
       wgrad(k + ".shortcut.conv", x, PRO_NONE, nullptr, dyf, 1, false, 1, true);
@@ -423,7 +434,7 @@ struct TrainPlan {
     T4 d = dxn;
     if (final_elu) {
       T4 d2 = like(dxn);
-      if (!dry) ok(elu_backward_post(dxn.p, S(k + ".out").p, nullptr, d2.p, n(d2), st), "elu_backward");
+      if (!dry) ok(elu_backward_post(dxn.p, S(k + ".out").p, nullptr, d2.p, n(d2), st, h16), "elu_backward");
       d = d2;
     }
     for (int i = nb - 1; i >= 0; --i) {
@@ -445,12 +456,13 @@ struct TrainPlan {
     T4 dp2 = like(X);
     dgrad(k + ".convs.1", dx2, dp2, 1, true, 3, 0, nullptr, nullptr, nullptr);
     T4 dpath1 = like(X);
-    if (!dry) ok(maxpool5_backward(idxs.at(k + ".i2"), dp2.p, dx2.p, dpath1.p, B, X.H, X.W, X.C, st), "maxpool5_backward");
+    if (!dry)
+      ok(maxpool5_backward(idxs.at(k + ".i2"), dp2.p, dx2.p, dpath1.p, B, X.H, X.W, X.C, st, h16), "maxpool5_backward");
     wgrad(k + ".convs.0", p1, PRO_NONE, nullptr, dpath1, 1, true, 3, false);
     T4 dp1 = like(X);
     dgrad(k + ".convs.0", dpath1, dp1, 1, true, 3, 0, nullptr, nullptr, nullptr);
     T4 dX = like(X);
-    if (!dry) ok(maxpool5_backward(idxs.at(k + ".i1"), dp1.p, dx2.p, dX.p, B, X.H, X.W, X.C, st), "maxpool5_backward");
+    if (!dry) ok(maxpool5_backward(idxs.at(k + ".i1"), dp1.p, dx2.p, dX.p, B, X.H, X.W, X.C, st, h16), "maxpool5_backward");
     return dX;
   }
   // returns the gradients of the refine block's inputs (second one empty for refine1)
@@ -460,11 +472,11 @@ struct TrainPlan {
     if (!two) return {rcub(k + ".adapt_convs.0", dX, 2, true), T4{}};
     const T4 &X = S(k + ".msf.X"), &hA = S(k + ".adapt_convs.0.out"), &hB = S(k + ".adapt_convs.1.out");
     T4 dm = like(X);
-    if (!dry) ok(elu_backward_post(dX.p, X.p, nullptr, dm.p, n(dm), st), "elu_backward");
+    if (!dry) ok(elu_backward_post(dX.p, X.p, nullptr, dm.p, n(dm), st, h16), "elu_backward");
     T4 dm1 = dm;
     if (hB.H != hA.H) {
       dm1 = mk(hB.H, hB.W, X.C);
-      if (!dry) ok(upsample_backward(dm.p, dm1.p, B, X.H, X.W, X.C, 0, st), "upsample_backward");
+      if (!dry) ok(upsample_backward(dm.p, dm1.p, B, X.H, X.W, X.C, 0, st, h16), "upsample_backward");
     }
     wgrad(k + ".msf.convs.0", hA, PRO_NONE, nullptr, dm, 1, true, 3, true);
     T4 dhA = like(hA);
@@ -498,7 +510,7 @@ struct TrainPlan {
     T4 g = like(o);
     if (!dry)
       ok(end_conv_backward(dscore, P("sigmas"), lab, P("end_conv.weight"), o.p, F("normalizer#ss"), g.p, epart,
-                           G("end_conv.weight"), G("end_conv.bias"), B, H, W, st),
+                           G("end_conv.weight"), G("end_conv.bias"), B, H, W, st, h16),
          "end_conv_backward");
     finished({"end_conv.weight", "end_conv.bias"});
     T4 d_o = like(o);
@@ -516,7 +528,7 @@ struct TrainPlan {
     d = resb("res1.1", d, false, 1, nullptr);
     d = resb("res1.0", d, false, 1, nullptr);
     if (!dry)
-      ok(begin_conv_wgrad(xin, d.p, epart, G("begin_conv.weight"), G("begin_conv.bias"), B, H, W, st),
+      ok(begin_conv_wgrad(xin, d.p, epart, G("begin_conv.weight"), G("begin_conv.bias"), B, H, W, st, h16),
          "begin_conv_wgrad");
     finished({"begin_conv.weight", "begin_conv.bias"});
     done_prefix = net->arena_floats;   // every gradient is final: the remaining buckets complete here
@@ -544,11 +556,13 @@ std::vector<std::string> grad_completion_order(sdp_net* net) {
 }
 
 static TrainPlan* plan_for(sdp_net* net, int B) {
-  if (net->plan && net->plan->B == B) return net->plan;
+  const bool h16 = net->mode == MODE_BF16 && net->tape16;
+  if (net->plan && net->plan->B == B && net->plan->h16 == h16) return net->plan;
   if (net->plan) destroy_plan(net->plan);
   TrainPlan* p = new TrainPlan();
   p->net = net;
   p->B = B;
+  p->h16 = h16;
   p->H = net->d.H;
   p->W = net->d.W;
   p->C = net->d.ngf;
@@ -583,6 +597,12 @@ static void enable_training(sdp_net* net, hipStream_t st) {
 }
 
 extern "C" {
+
+int sdp_net_set_tape(sdp_net* net, int bf16) {
+  if (!net || bf16 < 0 || bf16 > 1) return tfail("sdp_net_set_tape: bad argument");
+  net->tape16 = bf16 != 0;
+  return 0;
+}
 
 int sdp_net_train_workspace_size(sdp_net* net, int B, size_t* bytes) {
   if (!net || !bytes || B <= 0 || !net->finalized) return tfail("sdp_net_train_workspace_size: bad argument");

@@ -120,7 +120,8 @@ hipError_t pack_weights(const float* w, uint32_t* out, int Cout, int Cin, int k,
 // thread, so the reduce streams g and h at HBM rate while the finalize still sums only HW / 512
 // groups per image.
 constexpr int INPP_GRP = 512, INPP_NT = 1024;
-__global__ __launch_bounds__(INPP_NT) void inpp_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ h,
+template <typename TA>
+__global__ __launch_bounds__(INPP_NT) void inpp_bwd_reduce_kernel(const TA* __restrict__ g, const TA* __restrict__ h,
                                                                   const float4* __restrict__ nst, float2* __restrict__ part,
                                                                   int HW, int C) {
   __shared__ float2 red[INPP_NT * 4];
@@ -142,8 +143,8 @@ __global__ __launch_bounds__(INPP_NT) void inpp_bwd_reduce_kernel(const float* _
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const size_t o = base + (size_t)(pl + (j + u) * PL) * C + c4 * 4;
-      gv[u] = *reinterpret_cast<const float4*>(g + o);
-      hv[u] = *reinterpret_cast<const float4*>(h + o);
+      gv[u] = ldg4(g, o);
+      hv[u] = ldg4(h, o);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -248,9 +249,10 @@ __global__ void inpp_bwd_params_kernel(const float* __restrict__ ppart, int B, i
 
 // out = k1*g + k2*(h - mean) + k3 (+ r1) (+ r2).  Grid (blocks, B): a thread's channel group is
 // fixed (the block stride is a multiple of C/4), so its 4 coefficient rows are loaded once per image
-__global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ h,
-                                                             const float4* __restrict__ coef, const float* __restrict__ r1,
-                                                             const float* __restrict__ r2, float* __restrict__ out, int HW,
+template <typename TA>
+__global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const TA* __restrict__ g, const TA* __restrict__ h,
+                                                             const float4* __restrict__ coef, const TA* __restrict__ r1,
+                                                             const TA* __restrict__ r2, TA* __restrict__ out, int HW,
                                                              int C) {
   // (__restrict__ on every operand -- the calls are elementwise, so even an in-place one is safe --
   // lets the next iteration's loads issue before this one's store: loads and stores retire in order)
@@ -261,23 +263,21 @@ __global__ __launch_bounds__(256) void inpp_bwd_apply_kernel(const float* __rest
   const int c = (int)(i0 % C4) * 4;
   const float4* cf = coef + (size_t)b * C + c;
   const float4 k0 = cf[0], kk1 = cf[1], kk2 = cf[2], kk3 = cf[3];
-  const float4* g4 = reinterpret_cast<const float4*>(g) + off;
-  const float4* h4 = reinterpret_cast<const float4*>(h) + off;
-  float4* o4 = reinterpret_cast<float4*>(out) + off;
 #pragma unroll 2
   for (size_t i = i0; i < n4; i += stride) {
-    const float4 gv = g4[i], hv = h4[i];
+    const size_t e = (off + i) * 4;
+    const float4 gv = ldg4(g, e), hv = ldg4(h, e);
     float4 v = make_float4(fmaf(k0.x, gv.x, fmaf(k0.y, hv.x - k0.w, k0.z)), fmaf(kk1.x, gv.y, fmaf(kk1.y, hv.y - kk1.w, kk1.z)),
                            fmaf(kk2.x, gv.z, fmaf(kk2.y, hv.z - kk2.w, kk2.z)), fmaf(kk3.x, gv.w, fmaf(kk3.y, hv.w - kk3.w, kk3.z)));
     if (r1) {
-      const float4 t = reinterpret_cast<const float4*>(r1)[off + i];
+      const float4 t = ldg4(r1, e);
       v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
     }
     if (r2) {
-      const float4 t = reinterpret_cast<const float4*>(r2)[off + i];
+      const float4 t = ldg4(r2, e);
       v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
     }
-    o4[i] = v;
+    stg4(out, e, v);
   }
 }
 
@@ -287,12 +287,13 @@ static int grid_for(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 25
 // block's 1024 threads hold C/4 channel groups x 4096/C pixel lanes, C/4 must divide 256 (the apply
 // kernel's channel-fixed stride) and each lane's share of a 512-pixel group a multiple of 4
 // (C % 32 == 0); anything else returns hipErrorInvalidValue (kernels.h).
-hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
-                         int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
-                         float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st) {
+template <typename TA>
+static hipError_t inpp_backward_t(const TA* g, const TA* h, const float* nst, const float* alpha, const float* gamma,
+                                  int B, int HW, int C, float* part, float* coef, float* ppart, float* dalpha,
+                                  float* dgamma, float* dbeta, const TA* r1, const TA* r2, TA* out, hipStream_t st) {
   if (HW % INPP_GRP || C % 4 || C > 512 || (256 % (C / 4)) || (INPP_GRP / (INPP_NT / (C / 4))) % 4) return hipErrorInvalidValue;
   const int ngrp = HW / INPP_GRP;
-  hipLaunchKernelGGL(inpp_bwd_reduce_kernel, dim3(ngrp, B), dim3(INPP_NT), 0, st, g, h,
+  hipLaunchKernelGGL(inpp_bwd_reduce_kernel<TA>, dim3(ngrp, B), dim3(INPP_NT), 0, st, g, h,
                      reinterpret_cast<const float4*>(nst), reinterpret_cast<float2*>(part), HW, C);
   hipLaunchKernelGGL(inpp_bwd_finalize_kernel, dim3(B), dim3(1024), 0, st, reinterpret_cast<const float2*>(part), ngrp,
                      (float)HW, reinterpret_cast<const float4*>(nst), alpha, gamma, C, reinterpret_cast<float4*>(coef),
@@ -301,14 +302,24 @@ hipError_t inpp_backward(const float* g, const float* h, const float* nst, const
   // per image: 2048 blocks at most, the stride a multiple of C/4 (256 threads, C/4 divides 256)
   const size_t n4 = (size_t)HW * C / 4;
   const int nb = (int)std::min<size_t>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(inpp_bwd_apply_kernel, dim3(nb, B), dim3(256), 0, st, g, h,
+  hipLaunchKernelGGL(inpp_bwd_apply_kernel<TA>, dim3(nb, B), dim3(256), 0, st, g, h,
                      reinterpret_cast<const float4*>(coef), r1, r2, out, HW, C);
   return hipGetLastError();
 }
 
+hipError_t inpp_backward(const float* g, const float* h, const float* nst, const float* alpha, const float* gamma, int B,
+                         int HW, int C, float* part, float* coef, float* ppart, float* dalpha, float* dgamma,
+                         float* dbeta, const float* r1, const float* r2, float* out, hipStream_t st, bool h16) {
+  if (!h16) return inpp_backward_t(g, h, nst, alpha, gamma, B, HW, C, part, coef, ppart, dalpha, dgamma, dbeta, r1, r2, out, st);
+  auto H = [](const float* p) { return reinterpret_cast<const __bf16*>(p); };
+  return inpp_backward_t(H(g), H(h), nst, alpha, gamma, B, HW, C, part, coef, ppart, dalpha, dgamma, dbeta, H(r1), H(r2),
+                         reinterpret_cast<__bf16*>(out), st);
+}
+
 // ---------------------------------------------------------------- pooling / upsampling adjoints
 // ConvMeanPool: out = (o00 + o10 + o01 + o11)/4 -> d o_yx = dout[y/2][x/2] / 4   (dst full-res)
-__global__ void unpool_kernel(const float* __restrict__ dout, float* __restrict__ dst, int H, int W, int C, size_t n4) {
+template <typename TA>
+__global__ void unpool_kernel(const TA* __restrict__ dout, TA* __restrict__ dst, int H, int W, int C, size_t n4) {
   const int C4 = C / 4;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const int c4 = i % C4;
@@ -317,8 +328,8 @@ __global__ void unpool_kernel(const float* __restrict__ dout, float* __restrict_
     p /= W;
     const int y = p % H;
     const size_t b = p / H;
-    const float4 v = reinterpret_cast<const float4*>(dout)[((b * (H / 2) + y / 2) * (W / 2) + x / 2) * C4 + c4];
-    reinterpret_cast<float4*>(dst)[i] = make_float4(v.x * 0.25f, v.y * 0.25f, v.z * 0.25f, v.w * 0.25f);
+    const float4 v = ldg4(dout, (((b * (H / 2) + y / 2) * (W / 2) + x / 2) * C4 + c4) * 4);
+    stg4(dst, i * 4, make_float4(v.x * 0.25f, v.y * 0.25f, v.z * 0.25f, v.w * 0.25f));
   }
 }
 
@@ -329,8 +340,9 @@ __global__ void unpool_kernel(const float* __restrict__ dout, float* __restrict_
 // input byte is read from HBM ~1.1 times and each of the 25 checks per output reads LDS.
 // Positions outside the image get an index no window offset matches.
 constexpr int MPB_W = 32, MPB_CB = 32;
-__global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const float* __restrict__ dp, const uchar4* __restrict__ idx,
-                                                           const float* __restrict__ res, float* __restrict__ dst, int H,
+template <typename TA>
+__global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const TA* __restrict__ dp, const uchar4* __restrict__ idx,
+                                                           const TA* __restrict__ res, TA* __restrict__ dst, int H,
                                                            int W, int C, int rpb) {
   constexpr int C4B = MPB_CB / 4, PC = MPB_W + 4, RU = PC * C4B;   // 288 16-B units per ring row
   __shared__ float4 sd[5 * RU];
@@ -345,7 +357,6 @@ __global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const float* __restri
   const int chunk = t % nch;
   const size_t b = t / nch;
   const int y0 = chunk * rpb, y1 = min(H, y0 + rpb), x0 = tx * MPB_W, c40 = cb * C4B, C4 = C / 4;
-  const float4* dp4 = reinterpret_cast<const float4*>(dp);
   float4 d[2];
   uchar4 k[2];
   auto fetch = [&](int row) {
@@ -354,7 +365,7 @@ __global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const float* __restri
       const int u = tid + h * 256, xx = x0 - 2 + u / C4B;
       if (u < RU && row >= 0 && row < H && xx >= 0 && xx < W) {
         const size_t j = ((b * H + row) * W + xx) * C4 + c40 + u % C4B;
-        d[h] = dp4[j];
+        d[h] = ldg4(dp, j * 4);
         k[h] = idx[j];
       } else {
         d[h] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -384,7 +395,7 @@ __global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const float* __restri
     __syncthreads();
     fetch(y + 3);
     const size_t o = ((b * H + y) * W + x0 + col) * C4 + c40 + c4;
-    float4 s = res ? reinterpret_cast<const float4*>(res)[o] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 s = res ? ldg4(res, o * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int dy = -2; dy <= 2; ++dy) {
       int sl = base + dy + 2;
@@ -403,7 +414,7 @@ __global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const float* __restri
         }
       }
     }
-    reinterpret_cast<float4*>(dst)[o] = s;
+    stg4(dst, o * 4, s);
     base = base == 4 ? 0 : base + 1;
     __syncthreads();
   }
@@ -421,7 +432,8 @@ SDP_DEV void up_weights(int o, int n_lo, float scale, int* i0, int* i1, float* w
   *w0 = 1.f - *w1;
 }
 
-__global__ void upsample_bwd_kernel(const float* __restrict__ g, float* __restrict__ dlow, int H, int W, int C,
+template <typename TA>
+__global__ void upsample_bwd_kernel(const TA* __restrict__ g, TA* __restrict__ dlow, int H, int W, int C,
                                     int accumulate, size_t n4) {
   const int h = H / 2, w = W / 2, C4 = C / 4;
   const float sh = (float)(h - 1) / (float)(H - 1), sw = (float)(w - 1) / (float)(W - 1);
@@ -448,42 +460,43 @@ __global__ void upsample_bwd_kernel(const float* __restrict__ g, float* __restri
         up_weights(x, w, sw, &b0, &b1, &v0, &v1);
         const float wx = (b0 == j ? v0 : 0.f) + (b1 == j ? v1 : 0.f);
         if (wx == 0.f) continue;
-        const float4 gv = reinterpret_cast<const float4*>(g)[((b * H + y) * W + x) * C4 + c4];
+        const float4 gv = ldg4(g, (((b * H + y) * W + x) * C4 + c4) * 4);
         const float ww = wy * wx;
         s = make_float4(fmaf(ww, gv.x, s.x), fmaf(ww, gv.y, s.y), fmaf(ww, gv.z, s.z), fmaf(ww, gv.w, s.w));
       }
     }
-    float4* o = reinterpret_cast<float4*>(dlow) + i;
     if (accumulate) {
-      const float4 t = *o;
+      const float4 t = ldg4(dlow, i * 4);
       s = make_float4(s.x + t.x, s.y + t.y, s.z + t.z, s.w + t.w);
     }
-    *o = s;
+    stg4(dlow, i * 4, s);
   }
 }
 
 // dst = dy * elu'(from the ELU output y) (+ res)
-__global__ void elu_bwd_post_kernel(const float* __restrict__ dy, const float* __restrict__ y,
-                                    const float* __restrict__ res, float* __restrict__ dst, size_t n4) {
+template <typename TA>
+__global__ void elu_bwd_post_kernel(const TA* __restrict__ dy, const TA* __restrict__ y,
+                                    const TA* __restrict__ res, TA* __restrict__ dst, size_t n4) {
 #pragma unroll 2
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const float4 d = reinterpret_cast<const float4*>(dy)[i], yv = reinterpret_cast<const float4*>(y)[i];
+    const float4 d = ldg4(dy, i * 4), yv = ldg4(y, i * 4);
     float4 v = make_float4(d.x * elu_grad(yv.x, 2), d.y * elu_grad(yv.y, 2), d.z * elu_grad(yv.z, 2),
                            d.w * elu_grad(yv.w, 2));
     if (res) {
-      const float4 t = reinterpret_cast<const float4*>(res)[i];
+      const float4 t = ldg4(res, i * 4);
       v = make_float4(v.x + t.x, v.y + t.y, v.z + t.z, v.w + t.w);
     }
-    reinterpret_cast<float4*>(dst)[i] = v;
+    stg4(dst, i * 4, v);
   }
 }
 
 // dst = a + b (float4 lanes)
-__global__ void add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ dst, size_t n4) {
+template <typename TA>
+__global__ void add_kernel(const TA* __restrict__ a, const TA* __restrict__ b, TA* __restrict__ dst, size_t n4) {
 #pragma unroll 2
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
-    const float4 x = reinterpret_cast<const float4*>(a)[i], y = reinterpret_cast<const float4*>(b)[i];
-    reinterpret_cast<float4*>(dst)[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+    const float4 x = ldg4(a, i * 4), y = ldg4(b, i * 4);
+    stg4(dst, i * 4, make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w));
   }
 }
 
@@ -509,37 +522,55 @@ static hipError_t sum_rows(const float* part, int K, int n, int stride, float* o
   return hipGetLastError();
 }
 
-hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hipStream_t st) {
+#define SDP_H16(p) reinterpret_cast<const __bf16*>(p)
+#define SDP_H16W(p) reinterpret_cast<__bf16*>(p)
+hipError_t unpool(const float* dout, float* dst, int B, int H, int W, int C, hipStream_t st, bool h16) {
   const size_t n4 = (size_t)B * H * W * C / 4;
-  hipLaunchKernelGGL(unpool_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dout, dst, H, W, C, n4);
+  if (h16) hipLaunchKernelGGL(unpool_kernel<__bf16>, dim3(grid_for(n4)), dim3(256), 0, st, SDP_H16(dout), SDP_H16W(dst), H, W, C, n4);
+  else hipLaunchKernelGGL(unpool_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, st, dout, dst, H, W, C, n4);
   return hipGetLastError();
 }
 
 hipError_t maxpool5_backward(const uint8_t* idx, const float* dp, const float* res, float* dst, int B, int H, int W, int C,
-                             hipStream_t st) {
+                             hipStream_t st, bool h16) {
   if (W % MPB_W || C % MPB_CB) return hipErrorInvalidValue;
   const int strips = B * (W / MPB_W) * (C / MPB_CB);
   int rpb = H;                                  // split the rows only as far as needed to fill the chip
   while (rpb > 8 && (long)strips * ((H + rpb - 1) / rpb) < 2048) rpb = (rpb + 1) / 2;
   const int nb = strips * ((H + rpb - 1) / rpb);
-  hipLaunchKernelGGL(maxpool5_bwd_kernel, dim3(nb), dim3(256), 0, st, dp, reinterpret_cast<const uchar4*>(idx), res, dst,
-                     H, W, C, rpb);
+  if (h16)
+    hipLaunchKernelGGL(maxpool5_bwd_kernel<__bf16>, dim3(nb), dim3(256), 0, st, SDP_H16(dp), reinterpret_cast<const uchar4*>(idx),
+                       SDP_H16(res), SDP_H16W(dst), H, W, C, rpb);
+  else
+    hipLaunchKernelGGL(maxpool5_bwd_kernel<float>, dim3(nb), dim3(256), 0, st, dp, reinterpret_cast<const uchar4*>(idx), res,
+                       dst, H, W, C, rpb);
   return hipGetLastError();
 }
 
-hipError_t upsample_backward(const float* g, float* dlow, int B, int H, int W, int C, int accumulate, hipStream_t st) {
+hipError_t upsample_backward(const float* g, float* dlow, int B, int H, int W, int C, int accumulate, hipStream_t st, bool h16) {
   const size_t n4 = (size_t)B * (H / 2) * (W / 2) * C / 4;
-  hipLaunchKernelGGL(upsample_bwd_kernel, dim3(grid_for(n4)), dim3(256), 0, st, g, dlow, H, W, C, accumulate, n4);
+  if (h16)
+    hipLaunchKernelGGL(upsample_bwd_kernel<__bf16>, dim3(grid_for(n4)), dim3(256), 0, st, SDP_H16(g), SDP_H16W(dlow), H, W, C,
+                       accumulate, n4);
+  else
+    hipLaunchKernelGGL(upsample_bwd_kernel<float>, dim3(grid_for(n4)), dim3(256), 0, st, g, dlow, H, W, C, accumulate, n4);
   return hipGetLastError();
 }
 
-hipError_t elu_backward_post(const float* dy, const float* y, const float* res, float* dst, size_t n, hipStream_t st) {
-  hipLaunchKernelGGL(elu_bwd_post_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, dy, y, res, dst, n / 4);
+hipError_t elu_backward_post(const float* dy, const float* y, const float* res, float* dst, size_t n, hipStream_t st, bool h16) {
+  if (h16)
+    hipLaunchKernelGGL(elu_bwd_post_kernel<__bf16>, dim3(grid_for(n / 4)), dim3(256), 0, st, SDP_H16(dy), SDP_H16(y), SDP_H16(res),
+                       SDP_H16W(dst), n / 4);
+  else
+    hipLaunchKernelGGL(elu_bwd_post_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st, dy, y, res, dst, n / 4);
   return hipGetLastError();
 }
 
-hipError_t add_tensors(const float* a, const float* b, float* dst, size_t n, hipStream_t st) {
-  hipLaunchKernelGGL(add_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a, b, dst, n / 4);
+hipError_t add_tensors(const float* a, const float* b, float* dst, size_t n, hipStream_t st, bool h16) {
+  if (h16)
+    hipLaunchKernelGGL(add_kernel<__bf16>, dim3(grid_for(n / 4)), dim3(256), 0, st, SDP_H16(a), SDP_H16(b), SDP_H16W(dst), n / 4);
+  else
+    hipLaunchKernelGGL(add_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, st, a, b, dst, n / 4);
   return hipGetLastError();
 }
 
@@ -553,7 +584,8 @@ SDP_DEV float linspace01_t(int i, int n) {
 }
 
 constexpr int BW_ROWS = 32;
-__global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+template <typename TA>
+__global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restrict__ x, const TA* __restrict__ dy,
                                                           float* __restrict__ part, int H, int W) {
   __shared__ float sp[4][3][66];
   __shared__ float sd[64][129];
@@ -582,7 +614,7 @@ __global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restric
     }
     for (int i = tid; i < 64 * 32; i += 256) {
       const int px = i >> 5, c4 = i & 31;
-      const float4 v = *reinterpret_cast<const float4*>(dy + (((size_t)b * H + y) * W + x0 + px) * 128 + c4 * 4);
+      const float4 v = ldg4(dy, (((size_t)b * H + y) * W + x0 + px) * 128 + c4 * 4);
       sd[px][c4 * 4] = v.x; sd[px][c4 * 4 + 1] = v.y; sd[px][c4 * 4 + 2] = v.z; sd[px][c4 * 4 + 3] = v.w;
     }
     __syncthreads();
@@ -603,10 +635,11 @@ __global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restric
 }
 
 hipError_t begin_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int H, int W,
-                            hipStream_t st) {
+                            hipStream_t st, bool h16) {
   if (H % BW_ROWS || W % 64) return hipErrorInvalidValue;
   const int nb = B * (H / BW_ROWS) * (W / 64);
-  hipLaunchKernelGGL(begin_wgrad_kernel, dim3(nb), dim3(256), 0, st, x, dy, part, H, W);
+  if (h16) hipLaunchKernelGGL(begin_wgrad_kernel<__bf16>, dim3(nb), dim3(256), 0, st, x, SDP_H16(dy), part, H, W);
+  else hipLaunchKernelGGL(begin_wgrad_kernel<float>, dim3(nb), dim3(256), 0, st, x, dy, part, H, W);
   (void)sum_rows(part, nb, 128 * 36, 128 * 37, dw, st);
   return sum_rows(part + 128 * 36, nb, 128, 128 * 37, db, st);
 }
@@ -615,10 +648,11 @@ hipError_t begin_conv_wgrad(const float* x, const float* dy, float* part, float*
 // Forward (ncsnv2.py:510-516): out[b][co] = (conv3x3_zero(ELU(IN++(o)), W) + bias) / sigmas[y_b].
 // dend = dscore / sigmas[y_b].  Data gradient (to the ELU output) with the IN++/ELU derivative
 // applied (g = da * elu'(o*scale + shift)); weight and bias gradients.
+template <typename TA>
 __global__ __launch_bounds__(256) void end_dgrad_kernel(const float* __restrict__ dscore, const float* __restrict__ sigmas,
                                                         const int64_t* __restrict__ labels, const float* __restrict__ w,
-                                                        const float* __restrict__ o, const float* __restrict__ ss,
-                                                        float* __restrict__ g, int H, int W) {
+                                                        const TA* __restrict__ o, const float* __restrict__ ss,
+                                                        TA* __restrict__ g, int H, int W) {
   constexpr int C = 128;
   __shared__ float sd[2][3][66];
   __shared__ float sw[2 * C * 9];
@@ -649,16 +683,16 @@ __global__ __launch_bounds__(256) void end_dgrad_kernel(const float* __restrict_
         for (int k = 0; k < 4; ++k) da[k] = fmaf(dv, sw[(co * C + c4 * 4 + k) * 9 + tap], da[k]);
       }
     const size_t idx = (((size_t)b * H + y) * W + x0 + px) * C + c4 * 4;
-    const float4 h = *reinterpret_cast<const float4*>(o + idx);
+    const float4 h = ldg4(o, idx);
     const float z0 = fmaf(h.x, s0.x, s0.y), z1 = fmaf(h.y, s0.z, s0.w), z2 = fmaf(h.z, s1.x, s1.y), z3 = fmaf(h.w, s1.z, s1.w);
-    *reinterpret_cast<float4*>(g + idx) =
-        make_float4(da[0] * elu_grad(z0, 1), da[1] * elu_grad(z1, 1), da[2] * elu_grad(z2, 1), da[3] * elu_grad(z3, 1));
+    stg4(g, idx, make_float4(da[0] * elu_grad(z0, 1), da[1] * elu_grad(z1, 1), da[2] * elu_grad(z2, 1), da[3] * elu_grad(z3, 1)));
   }
 }
 
 constexpr int EW_ROWS = 32;
+template <typename TA>
 __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict__ dscore, const float* __restrict__ sigmas,
-                                                        const int64_t* __restrict__ labels, const float* __restrict__ o,
+                                                        const int64_t* __restrict__ labels, const TA* __restrict__ o,
                                                         const float* __restrict__ ss, float* __restrict__ part, int H,
                                                         int W) {
   constexpr int C = 128;
@@ -682,7 +716,7 @@ __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict_
       const int yy = y - 1 + rr, xx = x0 - 1 + cc;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-        const float4 h = *reinterpret_cast<const float4*>(o + (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
+        const float4 h = ldg4(o, (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
         const float4 s0 = *reinterpret_cast<const float4*>(ssb + c4 * 8), s1 = *reinterpret_cast<const float4*>(ssb + c4 * 8 + 4);
         v = make_float4(elu(fmaf(h.x, s0.x, s0.y)), elu(fmaf(h.y, s0.z, s0.w)), elu(fmaf(h.z, s1.x, s1.y)),
                         elu(fmaf(h.w, s1.z, s1.w)));
@@ -709,11 +743,18 @@ __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict_
 
 hipError_t end_conv_backward(const float* dscore, const float* sigmas, const int64_t* labels, const float* w,
                              const float* o, const float* ss, float* g, float* part, float* dw, float* db, int B, int H,
-                             int W, hipStream_t st) {
+                             int W, hipStream_t st, bool h16) {
   if (H % EW_ROWS || W % 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(end_dgrad_kernel, dim3(B * H * (W / 64)), dim3(256), 0, st, dscore, sigmas, labels, w, o, ss, g, H, W);
   const int nb = B * (H / EW_ROWS) * (W / 32);
-  hipLaunchKernelGGL(end_wgrad_kernel, dim3(nb), dim3(256), 0, st, dscore, sigmas, labels, o, ss, part, H, W);
+  if (h16) {
+    hipLaunchKernelGGL(end_dgrad_kernel<__bf16>, dim3(B * H * (W / 64)), dim3(256), 0, st, dscore, sigmas, labels, w,
+                       SDP_H16(o), ss, SDP_H16W(g), H, W);
+    hipLaunchKernelGGL(end_wgrad_kernel<__bf16>, dim3(nb), dim3(256), 0, st, dscore, sigmas, labels, SDP_H16(o), ss, part, H, W);
+  } else {
+    hipLaunchKernelGGL(end_dgrad_kernel<float>, dim3(B * H * (W / 64)), dim3(256), 0, st, dscore, sigmas, labels, w, o, ss, g,
+                       H, W);
+    hipLaunchKernelGGL(end_wgrad_kernel<float>, dim3(nb), dim3(256), 0, st, dscore, sigmas, labels, o, ss, part, H, W);
+  }
   (void)sum_rows(part, nb, 2 * 128 * 9, 2 * 128 * 9 + 2, dw, st);
   return sum_rows(part + 2 * 128 * 9, nb, 2, 2 * 128 * 9 + 2, db, st);
 }

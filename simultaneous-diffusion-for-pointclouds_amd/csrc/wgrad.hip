@@ -476,6 +476,235 @@ __global__ __launch_bounds__(256, OCC >= 2 ? 2 : 1) void conv_wgrad_kernel(Wgrad
 #endif
 }
 
+// The bf16 training tape (train.hip): input and dy stored as bf16 [pixel][C].  bf16 mode, two workgroups
+// per CU as OCC 3, but the dy tile needs no conversion: wave w lands its own operand plane [px][32 Cout]
+// (64-B rows) straight from the bf16 tensor by LDS-DMA (8 instructions of 16 pixels x 64 B), into a
+// double buffer, so tile t+1's dy lands under tile t's MFMAs; the input patch travels as 16-B units of
+// 8 channels (half the bytes of the fp32 patch) through registers for the prologue.  The bias gradient
+// sums each wave's own plane back from LDS (bf16 values, float sums).
+template <int TC, int KS>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_h16_kernel(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  using T = WgTile<TC, KS>;
+  constexpr int NT = KS * KS;
+  constexpr int NUA = (T::NPIX * 4 + 255) / 256;        // 16-B input units (8 bf16 channels) per thread
+  static_assert(2 * (2 * T::DY_PLANE + T::A_PLANE) <= 160 * 1024, "two workgroups per CU");
+  static_assert(TC % 16 == 0, "a 16-pixel dy group inside one tile row");
+  __shared__ __attribute__((aligned(16))) char lds[2 * T::DY_PLANE + T::A_PLANE];
+  char* const aL = lds + 2 * T::DY_PLANE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  auto tidx = [&]() __attribute__((always_inline)) {   // an opaque copy: thread-derived values recomputed per use
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    return t;
+  };
+  const int d = a.dil, Hs = a.H / d, Ws = a.W / d;
+  const int tiles_c = Ws / TC, tiles_rc = (Hs / T::TR) * tiles_c, tiles_img = tiles_rc * d * d;
+  const int total = a.B * tiles_img;
+  const int ncb = (a.Cin / 32) * (a.Cout / 128), G = gridDim.x;   // as conv_wgrad_kernel: channel blocks per XCD
+  const int q = (G & 7) ? (int)blockIdx.x : ((int)blockIdx.x & 7) * (G >> 3) + ((int)blockIdx.x >> 3);
+  const int S = G / ncb;
+  const int cb = q % ncb, cib = cb % (a.Cin / 32), cob = cb / (a.Cin / 32);
+  const int split = q / ncb;
+  const int t_begin = (int)((long long)total * split / S), t_end = (int)((long long)total * (split + 1) / S);
+  const int ci0 = cib * 32, co0 = cob * 128;
+  const int Cin = a.Cin, Cout = a.Cout;
+  const __bf16* in16 = reinterpret_cast<const __bf16*>(a.in);
+  const __bf16* dy16 = reinterpret_cast<const __bf16*>(a.dy);
+  const uint32_t img_dy_bytes = (uint32_t)a.H * a.W * Cout * 2, img_in_bytes = (uint32_t)a.H * a.W * Cin * 2;
+
+  f32x16 acc[NT];
+  static_for<0, NT>([&](auto i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  });
+  int tb = 0, tph_r = 0, tph_c = 0, tsr0 = 0, tsc0 = 0;
+  auto decode = [&](int t) {
+    tb = t / tiles_img;
+    int r = t - tb * tiles_img;
+    const int ph = r / tiles_rc;
+    r -= ph * tiles_rc;
+    tph_r = ph / d;
+    tph_c = ph - tph_r * d;
+    tsr0 = (r / tiles_c) * T::TR;
+    tsc0 = (r % tiles_c) * TC;
+  };
+  // dy tile of the decoded tile -> plane buffer `buf`: wave w lands Cout [co0 + 32w, +32) of the 128 pixels
+  auto dma_dy = [&](int buf) __attribute__((always_inline)) {
+    const int tl = tidx(), l = tl & 63, w = tl >> 6;
+    const int voff = ((((l >> 2) * d) * Cout) + 32 * w + (l & 3) * 8) * 2;
+    const i32x4 rs = buffer_desc(dy16 + (size_t)tb * a.H * a.W * Cout, img_dy_bytes);
+    const int base = (((tsr0 * d + tph_r) * a.W + tsc0 * d + tph_c) * Cout + co0) * 2;
+    const uint32_t l0 = (uint32_t)(uintptr_t)(lds + buf * T::DY_PLANE) + (uint32_t)__builtin_amdgcn_readfirstlane(w) * 8192u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int px0 = 16 * j, row = px0 / TC, col = px0 % TC;
+      dma16_lds_opaque(rs, l0 + j * 1024, voff, base + ((row * d) * a.W + col * d) * Cout * 2);
+    }
+  };
+  // input patch of the decoded tile -> registers (16 B = 8 channels per unit) + the prologue's (scale, shift)
+  uint4 ra[NUA];
+  float4 ssv[4];
+  bool interior = false;
+  auto load_a = [&]() __attribute__((always_inline)) {
+    const int tl = tidx();
+    if (a.pro_mode != PRO_NONE) {
+      const float* ssb = a.pro_ss + (size_t)tb * a.ss_bstride + (ci0 + (tl & 3) * 8) * 2;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ssv[k] = *reinterpret_cast<const float4*>(ssb + 4 * k);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ssv[k] = make_float4(1.f, 0.f, 1.f, 0.f);
+    }
+    const __amdgpu_buffer_rsrc_t irs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(in16 + (size_t)tb * a.H * a.W * Cin), 0, img_in_bytes, 0x00020000);
+    interior = tsr0 >= T::HALO && tsr0 + T::TR + T::HALO <= Hs && tsc0 >= T::HALO && tsc0 + TC + T::HALO <= Ws;
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    if (interior) {
+      const int ibase = __builtin_amdgcn_readfirstlane(
+          ((((tsr0 - T::HALO) * d + tph_r) * a.W + (tsc0 - T::HALO) * d + tph_c) * Cin + ci0) * 2);
+#pragma unroll
+      for (int k = 0; k < NUA; ++k) {
+        int u = tl + k * 256;
+        u = u < T::NPIX * 4 ? u : 0;
+        const int pix = u >> 2, cv = u & 3;
+        const int vo = (((pix / T::PC) * d * a.W + (pix % T::PC) * d) * Cin + cv * 8) * 2;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(irs, vo, ibase, 0);
+        ra[k] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < NUA; ++k) {
+      int u = tl + k * 256;
+      u = u < T::NPIX * 4 ? u : 0;
+      const int pix = u >> 2, cv = u & 3;
+      int sr = tsr0 - T::HALO + pix / T::PC, sc = tsc0 - T::HALO + pix % T::PC;
+      if (a.circular) {
+        sr = sr < 0 ? sr + Hs : (sr >= Hs ? sr - Hs : sr);
+        sc = sc < 0 ? sc + Ws : (sc >= Ws ? sc - Ws : sc);
+      } else {
+        sr = min(max(sr, 0), Hs - 1);
+        sc = min(max(sc, 0), Ws - 1);
+      }
+      const int y = sr * d + tph_r, x = sc * d + tph_c;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(irs, ((y * a.W + x) * Cin + ci0 + cv * 8) * 2, 0, 0);
+      ra[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  // registers -> aL [px][32 ci] bf16: prologue (IN++ affine + ELU, ELU), zero padding
+  auto store_a = [&]() __attribute__((always_inline)) {
+    const int tl = tidx();
+#pragma unroll
+    for (int k = 0; k < NUA; ++k) {
+      const int u = tl + k * 256;
+      if (u >= T::NPIX * 4) break;
+      const int pix = u >> 2, cv = u & 3;
+      const float4 lo = bf4_to_f4(make_uint2(ra[k].x, ra[k].y)), hi = bf4_to_f4(make_uint2(ra[k].z, ra[k].w));
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      if (a.pro_mode != PRO_NONE) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float4 sv = ssv[e >> 1];
+          v[e] = elu(fmaf(v[e], (e & 1) ? sv.z : sv.x, (e & 1) ? sv.w : sv.y));
+        }
+      }
+      if (!a.circular && KS == 3) {
+        const int sr = tsr0 - 1 + pix / T::PC, sc = tsc0 - 1 + pix % T::PC;
+        if (sr < 0 || sr >= Hs || sc < 0 || sc >= Ws) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = 0.f;
+        }
+      }
+      *reinterpret_cast<uint4*>(aL + pix * 64 + cv * 16) =
+          make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+    }
+  };
+  // bias gradient: this lane's 8 channels ((lane & 3) * 8 of the wave's 32) summed over its pixels
+  float bs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = a.bpart && cib == 0;
+  auto bias_sum = [&](int buf) __attribute__((always_inline)) {
+    const char* p = lds + buf * T::DY_PLANE + wave * 8192 + lane * 16;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint4 u = *reinterpret_cast<const uint4*>(p + j * 1024);
+      const float4 lo = bf4_to_f4(make_uint2(u.x, u.y)), hi = bf4_to_f4(make_uint2(u.z, u.w));
+      bs[0] += lo.x; bs[1] += lo.y; bs[2] += lo.z; bs[3] += lo.w;
+      bs[4] += hi.x; bs[5] += hi.y; bs[6] += hi.z; bs[7] += hi.w;
+    }
+  };
+  // the MFMAs of the staged tile (as conv_wgrad_kernel, bf16 mode)
+  auto compute = [&](const char* dyb) __attribute__((always_inline)) {
+    const int tl = tidx(), ln = tl & 63;
+    const int Gq = ln >> 4, qq = (ln & 15) >> 2, p = ln & 3;
+    const int kq = 8 * (Gq >> 1) + qq;
+    const int mcol = 16 * (Gq & 1) + 4 * p;
+    const char* dy_rd = dyb + __builtin_amdgcn_readfirstlane(tl >> 6) * (128 * 64) + mcol * 2;
+    const char* a_rd = aL + mcol * 2;
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {
+      const int k0 = 16 * s + kq, k1 = k0 + 4;
+      const bf16x8 ahi = cat8(ds_read_tr(dy_rd + k0 * 64), ds_read_tr(dy_rd + k1 * 64));
+      const int p0 = (k0 / TC) * T::PC + k0 % TC, p1 = (k1 / TC) * T::PC + k1 % TC;
+      const char* b0 = a_rd + p0 * 64;
+      const char* b1 = a_rd + p1 * 64;
+      auto rd_b = [&](int toff) { return cat8(ds_read_tr(b0 + toff), ds_read_tr(b1 + toff)); };
+      bf16x8 bhi_n = rd_b(0);
+      static_for<0, NT>([&](auto tc_) {
+        constexpr int tap = decltype(tc_)::value;
+        const bf16x8 bhi = bhi_n;
+        if constexpr (tap + 1 < NT) {
+          constexpr int toff = (KS == 3 ? ((tap + 1) / 3) * T::PC + (tap + 1) % 3 : 0) * 64;
+          bhi_n = rd_b(toff);
+        }
+        acc[tap] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[tap], 0, 0, 0);
+      });
+    }
+  };
+  int buf = 0;
+  if (t_begin < t_end) {
+    decode(t_begin);
+    dma_dy(0);
+  }
+  for (int t = t_begin; t < t_end; ++t) {
+    load_a();                                            // tile t's input patch, beside its dy DMA
+    __builtin_amdgcn_s_waitcnt(0x0070);                  // vmcnt(0) + lgkmcnt(0): dy landed, patch in registers
+    store_a();
+    if (do_bias) bias_sum(buf);                          // this wave's own plane (its own DMA, waited above)
+    __syncthreads();                                     // aL complete
+    if (t + 1 < t_end) {
+      decode(t + 1);
+      dma_dy(buf ^ 1);                                   // lands under this tile's MFMAs
+    }
+    compute(lds + buf * T::DY_PLANE);
+    __syncthreads();                                     // aL and this plane buffer read before they are rewritten
+    buf ^= 1;
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = bs[e];
+      v += __shfl_xor(v, 4);
+      v += __shfl_xor(v, 8);
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+      bs[e] = v;
+    }
+    if (lane < 4) {
+      float* bp = a.bpart + (size_t)split * Cout + co0 + wave * 32 + lane * 8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bp[e] = bs[e];
+    }
+  }
+  static_for<0, NT>([&](auto tc_) {
+    constexpr int tap = decltype(tc_)::value;
+    float* dst = a.part + (((size_t)split * NT + tap) * Cout + co0 + wave * 32) * Cin + ci0 + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dst[(size_t)((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * Cin] = acc[tap][r];
+  });
+#endif
+}
+
 // out[co][ci][tap] (+)= sum_s part[s][tap][co][ci] (fixed order over s); grid.y = tap, and
 // grid.y == NT reduces the bias partials bpart[s][co] into bias_out
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ part,
@@ -561,7 +790,7 @@ static hipError_t wgrad_mode(const WgradArgs& a, int ks, int tc, int S, hipStrea
 }
 
 hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out, int accumulate, hipStream_t st,
-                      const char** why) {
+                      const char** why, bool h16) {
   const int d = a.dil;
   if (a.Cin % 32 || a.Cout % 128) { *why = "wgrad: Cin%32 and Cout%128 required"; return hipErrorInvalidValue; }
   if (a.H % d || a.W % d) { *why = "wgrad: H,W must be multiples of the dilation"; return hipErrorInvalidValue; }
@@ -579,7 +808,14 @@ hipError_t conv_wgrad(int mode, WgradArgs a, int ks, float* out, float* bias_out
     return hipErrorInvalidValue;
   }
   hipError_t e;
-  switch (mode) {
+  if (h16) {   // the bf16 tape: 4 x 32 tiles (3x3) or 2 x 64 (1x1)
+    if (mode != MODE_BF16) { *why = "wgrad: the bf16 tape runs in bf16 mode"; return hipErrorInvalidValue; }
+    const dim3 grid(S * (a.Cin / 32) * (a.Cout / 128));
+    if (ks == 1) hipLaunchKernelGGL((conv_wgrad_h16_kernel<64, 1>), grid, dim3(256), 0, st, a);
+    else if (Ws % 32 == 0 && Hs % 4 == 0) hipLaunchKernelGGL((conv_wgrad_h16_kernel<32, 3>), grid, dim3(256), 0, st, a);
+    else { *why = "wgrad: the bf16 tape needs 4 x 32 tiles"; return hipErrorInvalidValue; }
+    e = hipGetLastError();
+  } else switch (mode) {
     case MODE_F32X3: e = wgrad_mode<MODE_F32X3>(a, ks, tc, S, st); break;
     case MODE_BF16: e = wgrad_mode<MODE_BF16>(a, ks, tc, S, st); break;
     default: *why = "wgrad: training runs in fp32x3 or bf16"; return hipErrorInvalidValue;

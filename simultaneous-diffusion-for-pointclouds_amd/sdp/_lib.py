@@ -50,6 +50,7 @@ _SIGS = {
     "sdp_net_forward": (I, [P, P, P, P, I, P, SZ, P]),
     "sdp_net_forward_langevin": (I, [P, P, P, I, C.POINTER(LangevinParams), P, SZ, P]),
     "sdp_net_set_split": (I, [P, I]),
+    "sdp_net_set_tape": (I, [P, I]),
     "sdp_net_destroy": (I, [P]),
     "sdp_net_profile_enable": (I, [P, I]),
     "sdp_net_profile_read": (I, [P, C.c_char_p, SZ, C.POINTER(I)]),

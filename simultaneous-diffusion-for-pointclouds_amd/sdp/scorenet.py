@@ -126,6 +126,11 @@ class ScoreNet:
         _lib.check(_lib.lib().sdp_net_set_split(self._h, int(ways)), "set_split")
         self._ws.clear()                    # the workspace size depends on it
 
+    def set_tape(self, bf16: bool):
+        """bf16 precision, training: keep the tape (activations, output gradients) in bf16 (True, the
+        default) or float32 (False).  Parameters, gradients and scores stay float32 either way."""
+        _lib.check(_lib.lib().sdp_net_set_tape(self._h, 1 if bf16 else 0), "set_tape")
+
     # ------------------------------------------------------------------ measurement
     def profile(self, enable: bool = True):
         _lib.check(_lib.lib().sdp_net_profile_enable(self._h, 1 if enable else 0), "profile_enable")

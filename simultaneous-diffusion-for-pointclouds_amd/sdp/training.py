@@ -40,9 +40,13 @@ class Trainer:
     def __init__(self, net: ScoreNet, lr: float = 1e-4, beta1: float = 0.9, beta2: float = 0.999,
                  eps: float = 1e-8, ema: bool = True, ema_mu: float = 0.999, device="cuda", dist_group=None,
                  optimizer: str = "Adam", weight_decay: float = 0.0, amsgrad: bool = False,
-                 alpha: float = 0.99, momentum: float = 0.9, grad_wire_dtype=None, bucket_floats=None):
+                 alpha: float = 0.99, momentum: float = 0.9, grad_wire_dtype=None, bucket_floats=None,
+                 tape_bf16: bool = True):
         if net.precision not in ("fp32x3", "bf16"):
             raise ValueError("training runs in precision fp32x3 or bf16")
+        # bf16 precision: the tape (activations, output gradients) in bf16 (sdp_net_set_tape); fp32x3 keeps
+        # float32 tensors whatever this says
+        net.set_tape(tape_bf16)
         if optimizer not in self.OPTIMIZERS:
             raise NotImplementedError("Optimizer {} not understood.".format(optimizer))   # losses/__init__.py:12-13
         L = _lib.lib()
@@ -105,6 +109,11 @@ class Trainer:
         return {k: v.detach().clone() for k, v in self.named_parameters(self.shadow)}
 
     # ------------------------------------------------------------------ forward / loss / backward
+    def set_tape(self, bf16: bool):
+        """Switch the bf16 tape on or off (bf16 precision); the next forward re-sizes the workspace."""
+        self.net.set_tape(bf16)
+        self._ws.clear()
+
     def _workspace(self, B):
         ws = self._ws.get(B)
         if ws is None:

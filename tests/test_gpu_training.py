@@ -109,6 +109,32 @@ def test_bf16_training_gradients_close(case):
     print("bf16 gradient norm-rel error, worst:", [(k, f"{nrel[k]:.2e}") for k in worst])
 
 
+def test_bf16_tape_matches_float32_tape(case):
+    """The bf16 tape (every activation and output gradient stored once in bf16: sdp_net_set_tape, the
+    bf16-mode default) against the same bf16-mode backward on a float32 tape: the only difference is
+    the rounding of the stored tensors, so every parameter's gradient must keep cosine >= 0.995 and the
+    loss 1e-2 (a wrong index in any bf16-tensor kernel drops its layers' cosines far below that)."""
+    def run(tape):
+        net = ScoreNet(H=H, W=W, precision="bf16").load_synthetic()
+        tr = Trainer(net, tape_bf16=tape)
+        dev = "cuda"
+        loss, scores = anneal_dsm_score_estimation_with_mask(tr, case["X"].to(dev), case["used"].to(dev),
+                                                             case["noise"].to(dev), case["mask"].to(dev), None,
+                                                             net.sigmas.to(dev), case["labels"].to(dev))
+        tr.backward()
+        torch.cuda.synchronize()
+        return loss.item(), scores.cpu(), {k: g.cpu().clone() for k, g in tr.named_grads()}
+    l16, s16, g16 = run(True)
+    l32, s32, g32 = run(False)
+    serr = ((s16 - s32).abs().max() / s32.abs().max()).item()
+    cos = {k: torch.nn.functional.cosine_similarity(g16[k].flatten(), g32[k].flatten(), dim=0).item() for k in g32}
+    worst = sorted(cos, key=lambda k: cos[k])[:8]
+    print(f"bf16 tape vs float32 tape: loss {l16:.6g} vs {l32:.6g}, scores max err {serr:.2e}; lowest cosines:",
+          [(k, f"{cos[k]:.5f}") for k in worst])
+    assert abs(l16 - l32) <= 1e-2 * abs(l32)
+    assert min(cos.values()) >= 0.995, [(k, cos[k]) for k in worst]
+
+
 def test_bf16_gradients_full_size_against_fp32x3():
     """The bf16 training backward at the bench's size (64 x 1024, B = 8: every conv's full-size tiling,
     the weight gradients' whole split range) against the fp32x3 backward of the same batch, which
