@@ -149,6 +149,9 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   constexpr int CPU = IO16 ? 8 : 4;                // channels per 16-B staging unit
   constexpr int USH = IO16 ? 2 : 3;                // log2(staging units per pixel-chunk)
   constexpr int PPU = CPU / 2;                     // 2-channel transform pieces per unit
+  // IO16 without an ELU prologue (the data gradient, the CRP / MSF / shortcut convs: the identity (1, 0)
+  // table): the transform is a copy of the unit's 16 B (zero padding aside)
+  constexpr bool COPY = IO16 && !PELU;
   static_assert((SH == 32) == (MODE == MODE_F32), "bf16 modes: 16x16 shape; exact fp32: 32x32");
   static_assert(NW == 4 || (SH == 16 && !POOL), "2-wave workgroups: the 16x16 non-pooled forward only");
   static_assert(NJ == 4 || (SH == 16 && !POOL && KS == 3 && WM == 1), "32-Cout waves: the 16x16 3x3 tiles only");
@@ -351,6 +354,14 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     constexpr int k = decltype(kc)::value;
     constexpr int PB = decltype(pb)::value;
     const int pix = (tid + k * NTH) >> USH;   // units past the patch land in its slack: no branch
+    if constexpr (COPY) {
+      uint4 u = __builtin_bit_cast(uint4, v);
+      if constexpr (ZP) {
+        if (!((uvalid >> k) & 1u)) u = make_uint4(0u, 0u, 0u, 0u);
+      }
+      *reinterpret_cast<uint4*>(lds + PB * T::PATCH_BYTES + pix * PSTRIDE + my_cv * 16) = u;
+      return;
+    }
     if constexpr (IO16) {   // 8 bf16 channels -> prologue -> 8 bf16 (one 16-B LDS write)
       const uint4 u = __builtin_bit_cast(uint4, v);
       const float4 lo = bf4_to_f4(make_uint2(u.x, u.y)), hi = bf4_to_f4(make_uint2(u.z, u.w));
@@ -577,9 +588,13 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
               acc4[mb][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bhi, acc4[mb][nj], 0, 0, 0);
             }
           }
-          if constexpr (blk < PPU * NX) xform_piece(std::integral_constant<int, tap + XT * (blk / PPU)>{},
-                                                    std::integral_constant<int, blk % PPU>{},
-                                                    std::integral_constant<int, 1 - P>{}, xv[blk / PPU]);
+          if constexpr (COPY) {
+            if constexpr (blk < NX) xform_store(std::integral_constant<int, tap + XT * blk>{}, std::integral_constant<int, 1 - P>{},
+                                                xv[blk]);
+          } else if constexpr (blk < PPU * NX) {
+            xform_piece(std::integral_constant<int, tap + XT * (blk / PPU)>{}, std::integral_constant<int, blk % PPU>{},
+                        std::integral_constant<int, 1 - P>{}, xv[blk / PPU]);
+          }
           __builtin_amdgcn_sched_barrier(0);
         });
         if constexpr (NT == 1) dmas();
@@ -640,7 +655,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
     static_for<0, NT>([&](auto tap_c) {
       constexpr int tap = decltype(tap_c)::value;
       constexpr int CUR = tap % 3, NXT = (tap + 2) % 3;
-      constexpr int U0 = XP::first(tap), UN = XP::count(tap), Q = UN * PPU * XP::NSTG;
+      constexpr int U0 = XP::first(tap), UN = XP::count(tap), Q = COPY ? UN : UN * PPU * XP::NSTG;
       constexpr int UNA = UN > 0 ? UN : 1;
       const int wchunk = tap + 2 < NT ? chunk : min(chunk + 1, nchunks - 1);
       constexpr int wtap = tap + 2 < NT ? tap + 2 : tap + 2 - NT;
@@ -653,6 +668,11 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
         constexpr int pc = decltype(pc_c)::value, st = decltype(st_c)::value;
         constexpr int j = pc / PPU, h = pc % PPU, k = U0 + j, PB = 1 - P;
         if constexpr (SDP_KO & 2) return;
+        if constexpr (COPY) {   // one stage per unit: the 16-B copy (stage q = unit q of the tap)
+          xform_store(std::integral_constant<int, U0 + decltype(pc_c)::value>{}, std::integral_constant<int, PB>{},
+                      xr[decltype(pc_c)::value]);
+          return;
+        }
         // the piece's two raw values (IO16: the bf16 halves of word h of the unit)
         auto raw2 = [&](float& r0, float& r1) __attribute__((always_inline)) {
           const float4 v = xr[j];
@@ -781,8 +801,10 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
         }
         static_for<0, Q>([&](auto q_c) {   // transform stages dealt to this block
           constexpr int q = decltype(q_c)::value;
-          if constexpr (XP::stage_blk(q, Q, NBLK) == blk)
-            stage(std::integral_constant<int, q / XP::NSTG>{}, std::integral_constant<int, q % XP::NSTG>{});
+          if constexpr (XP::stage_blk(q, Q, NBLK) == blk) {
+            if constexpr (COPY) stage(std::integral_constant<int, q>{}, std::integral_constant<int, 0>{});
+            else stage(std::integral_constant<int, q / XP::NSTG>{}, std::integral_constant<int, q % XP::NSTG>{});
+          }
         });
         if constexpr (UN > 0 && blk >= NBLK - UN)   // the DMA of a transformed unit (its raw slot was read)
           load_unit_o(std::integral_constant<int, U0 + blk - (NBLK - UN)>{}, chunk + 2);

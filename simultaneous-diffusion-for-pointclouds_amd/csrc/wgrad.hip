@@ -661,13 +661,15 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_h16_kernel(WgradArgs a) {
       });
     }
   };
+  // tile t+1's dy (LDS-DMA into the other plane buffer) and input patch (registers) are both issued
+  // before tile t's MFMAs, so a tile's only exposed wait is the one at the top of its iteration
   int buf = 0;
   if (t_begin < t_end) {
     decode(t_begin);
     dma_dy(0);
+    load_a();
   }
   for (int t = t_begin; t < t_end; ++t) {
-    load_a();                                            // tile t's input patch, beside its dy DMA
     __builtin_amdgcn_s_waitcnt(0x0070);                  // vmcnt(0) + lgkmcnt(0): dy landed, patch in registers
     store_a();
     if (do_bias) bias_sum(buf);                          // this wave's own plane (its own DMA, waited above)
@@ -675,6 +677,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_h16_kernel(WgradArgs a) {
     if (t + 1 < t_end) {
       decode(t + 1);
       dma_dy(buf ^ 1);                                   // lands under this tile's MFMAs
+      load_a();                                          // in flight under them too
     }
     compute(lds + buf * T::DY_PLANE);
     __syncthreads();                                     // aL and this plane buffer read before they are rewritten
