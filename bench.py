@@ -200,6 +200,37 @@ def conv_clock(cls):
     return None
 
 
+def split_overlap():
+    """Per memory-bound kernel class, the fraction of its time that ran under a conv of the OTHER forward
+    stream in the default two-stream step (tools/overlap.py over a rocprofv3 --kernel-trace of
+    `bench.py`, --split 2 -> profiles/rNN_overlap.json, newest first), keyed by the libsdp source hash
+    (sdp/_build.py source_hash): None when no file matches the current tree.  The per-kernel durations
+    above come from a profiled pass with one launch per layer; this says how much of that time the
+    default schedule hides."""
+    import glob
+    from sdp import _build
+    for fn in sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]_overlap.json")), reverse=True):
+        try:
+            with open(fn) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if isinstance(d, dict) and d.get("libsdp_source_hash") == _build.source_hash():
+            return d.get("classes", {}), os.path.basename(fn)
+    return None, None
+
+
+def overlap_of(kernel, classes):
+    keys = {"inpp_finalize": ("inpp_moments", "inpp_ss"), "maxpool5": ("maxpool5",), "begin_conv": ("begin_conv",),
+            "end_conv": ("end_conv+langevin",), "avgpool2": ("avgpool2",)}
+    for prefix, cl in keys.items():
+        if kernel.startswith(prefix):
+            tot = sum(classes[c]["total_us"] for c in cl if c in classes)
+            hid = sum(classes[c]["hidden_us"] for c in cl if c in classes)
+            return round(hid / tot, 4) if tot else None
+    return None
+
+
 # ----------------------------------------------------------------------------- timing harness
 def timed(step, args, dist, dev):
     for i in range(args.warmup):
@@ -382,12 +413,17 @@ def run_sampling(args, rank, N, dist, dev):
         # memory-bound kernels of the forward against the HBM roofline (north_star): algorithmic
         # bytes per launch / average launch time, HIP events on the forward's stream
         mem = []
+        ov_classes, ov_src = split_overlap() if args.workload == "line" else (None, None)
         for k, (n_, ms_, fl_, by_) in sorted(prof.items(), key=lambda kv: -kv[1][1]):
             if fl_ == 0 and by_ > 0:
                 t_ = ms_ / n_ / 1e3
                 mem.append({"kernel": k, "launches_per_step": round(n_ / steps, 2), "avg_launch_us": round(t_ * 1e6, 2),
                             "algorithmic_bytes": int(by_), "achieved_GBps": round(by_ / t_ / 1e9, 1),
                             "frac": round(by_ / t_ / 1e9 / HBM_PEAK, 4)})
+                if ov_classes is not None:
+                    hf = overlap_of(k, ov_classes)
+                    if hf is not None:
+                        mem[-1].update(hidden_frac_split2=hf, hidden_source=ov_src)
         mem.append({"kernel": "consistency_merge (7 kernels, HIP events around sdp_consistency_merge)",
                     "launches_per_step": 1, "avg_launch_us": round(merge_us, 2), "algorithmic_bytes": int(merge_bytes),
                     "achieved_GBps": round(merge_bytes / (merge_us * 1e-6) / 1e9, 1),

@@ -818,7 +818,10 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   static_assert(NT % 2 == 1, "parity bookkeeping assumes an odd tap count");
   // (the data-gradient launches keep do_chunk: in bf16 training the tap schedule measured 3-5 % slower
   // on them, profiles/experiments/r05_train_kernel_stats_ab.log)
-  if constexpr (MODE != MODE_F32 && NT == 9 && !TRANS) {
+#ifndef SDP_DGRAD16_TAPS   // A/B (build-time): the IO16 data gradient on the tap schedule -- measured slower,
+#define SDP_DGRAD16_TAPS 0    // bf16-tape training 181.0-181.5 -> 177.6-177.8 image-steps/s (profiles/experiments/r06_dgrad16_taps_ab.log)
+#endif
+  if constexpr (MODE != MODE_F32 && NT == 9 && (!TRANS || (IO16 && SDP_DGRAD16_TAPS))) {
     static_assert(XP::max_count() * PPU * XP::NSTG <= 2 * (NBLK - 2), "at most two transform stages per block");
     for (int chunk = 0; chunk < nchunks; chunk += 2) {   // nchunks is even (Cin % 64 == 0)
       do_chunk9(std::integral_constant<int, 0>{}, chunk);

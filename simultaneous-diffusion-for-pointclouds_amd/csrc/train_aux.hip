@@ -420,6 +420,101 @@ __global__ __launch_bounds__(256) void maxpool5_bwd_kernel(const TA* __restrict_
   }
 }
 
+// The bf16-tape form of maxpool5_bwd_kernel: 8-channel units (16 B of dp, 8 B of indices) -- each of the 25
+// window checks reads one 8-byte index word from LDS for 8 channels (a SWAR byte compare) instead of one
+// 4-byte word per 4 channels -- over 32-column x 64-channel strips, otherwise the same ring walk, the same
+// fixed summation order (dy, dx), so the result is deterministic.
+constexpr int MPH_W = 32, MPH_C = 64;
+__global__ __launch_bounds__(256) void maxpool5_bwd_h16_kernel(const __bf16* __restrict__ dp, const uint8_t* __restrict__ idx,
+                                                               const __bf16* __restrict__ res, __bf16* __restrict__ dst,
+                                                               int H, int W, int C, int rpb) {
+  constexpr int C8B = MPH_C / 8, PC = MPH_W + 4, RU = PC * C8B;   // 288 units per ring row
+  __shared__ uint4 sd[5 * RU];
+  __shared__ uint2 si[5 * RU];
+  const int tid = threadIdx.x;
+  const int tw = W / MPH_W, tc = C / MPH_C, nch = (H + rpb - 1) / rpb;
+  int t = blockIdx.x;
+  const int cb = t % tc;
+  t /= tc;
+  const int tx = t % tw;
+  t /= tw;
+  const int chunk = t % nch;
+  const size_t b = t / nch;
+  const int y0 = chunk * rpb, y1 = min(H, y0 + rpb), x0 = tx * MPH_W;
+  uint4 d[2];
+  uint2 k[2];
+  auto fetch = [&](int row) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + h * 256, xx = x0 - 2 + u / C8B;
+      if (u < RU && row >= 0 && row < H && xx >= 0 && xx < W) {
+        const size_t e = ((b * H + row) * W + xx) * C + cb * MPH_C + (u % C8B) * 8;
+        d[h] = *reinterpret_cast<const uint4*>(dp + e);
+        k[h] = *reinterpret_cast<const uint2*>(idx + e);
+      } else {
+        d[h] = make_uint4(0u, 0u, 0u, 0u);
+        k[h] = make_uint2(0xffffffffu, 0xffffffffu);   // no window offset matches
+      }
+    }
+  };
+  auto put = [&](int slot) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = tid + h * 256;
+      if (u < RU) {
+        sd[slot * RU + u] = d[h];
+        si[slot * RU + u] = k[h];
+      }
+    }
+  };
+  for (int r = 0; r < 4; ++r) {
+    fetch(y0 - 2 + r);
+    put(r);
+  }
+  fetch(y0 + 2);
+  const int c8 = tid % C8B, col = tid / C8B;   // 32 columns x 8 channel units
+  int base = 0;
+  for (int y = y0; y < y1; ++y) {
+    put(base == 0 ? 4 : base - 1);
+    __syncthreads();
+    fetch(y + 3);
+    const size_t o = ((b * H + y) * W + x0 + col) * C + cb * MPH_C + c8 * 8;
+    float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (res) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(res + o);
+      const float4 lo = bf4_to_f4(make_uint2(rv.x, rv.y)), hi = bf4_to_f4(make_uint2(rv.z, rv.w));
+      s[0] = lo.x; s[1] = lo.y; s[2] = lo.z; s[3] = lo.w; s[4] = hi.x; s[5] = hi.y; s[6] = hi.z; s[7] = hi.w;
+    }
+#pragma unroll
+    for (int dy = -2; dy <= 2; ++dy) {
+      int sl = base + dy + 2;
+      sl = sl >= 5 ? sl - 5 : sl;
+#pragma unroll
+      for (int dx = -2; dx <= 2; ++dx) {
+        const int u = sl * RU + (col + 2 + dx) * C8B + c8;
+        const uint2 kk = si[u];
+        const uint32_t want = (uint32_t)((2 - dy) * 5 + (2 - dx)) * 0x01010101u;
+        const uint32_t e0 = kk.x ^ want, e1 = kk.y ^ want;   // zero bytes where the index matches
+        const uint32_t z0 = (e0 - 0x01010101u) & ~e0 & 0x80808080u, z1 = (e1 - 0x01010101u) & ~e1 & 0x80808080u;
+        if (z0 | z1) {
+          const uint4 dd = sd[u];
+          const uint32_t w[4] = {dd.x, dd.y, dd.z, dd.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t byte = ((e < 4 ? kk.x : kk.y) >> (8 * (e & 3))) & 0xffu;
+            const float v = (e & 1) ? __uint_as_float(w[e >> 1] & 0xffff0000u) : __uint_as_float(w[e >> 1] << 16);
+            if (byte == ((2 - dy) * 5 + (2 - dx))) s[e] += v;
+          }
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dst + o) = make_uint4(pack_bf2(s[0], s[1]), pack_bf2(s[2], s[3]), pack_bf2(s[4], s[5]),
+                                                     pack_bf2(s[6], s[7]));
+    base = base == 4 ? 0 : base + 1;
+    __syncthreads();
+  }
+}
+
 // adjoint of the bilinear align_corners upsample [h][w] -> [H][W] (forward: conv epilogue `up`):
 // dlow[i][j] += sum_{y,x} wy(y,i) wx(x,j) g[y][x]  (gather over the few y, x that reach (i, j))
 SDP_DEV void up_weights(int o, int n_lo, float scale, int* i0, int* i1, float* w0, float* w1) {
@@ -538,10 +633,14 @@ hipError_t maxpool5_backward(const uint8_t* idx, const float* dp, const float* r
   int rpb = H;                                  // split the rows only as far as needed to fill the chip
   while (rpb > 8 && (long)strips * ((H + rpb - 1) / rpb) < 2048) rpb = (rpb + 1) / 2;
   const int nb = strips * ((H + rpb - 1) / rpb);
-  if (h16)
-    hipLaunchKernelGGL(maxpool5_bwd_kernel<__bf16>, dim3(nb), dim3(256), 0, st, SDP_H16(dp), reinterpret_cast<const uchar4*>(idx),
-                       SDP_H16(res), SDP_H16W(dst), H, W, C, rpb);
-  else
+  if (h16) {
+    if (C % MPH_C) return hipErrorInvalidValue;
+    const int strips16 = B * (W / MPH_W) * (C / MPH_C);
+    int rpb16 = H;
+    while (rpb16 > 8 && (long)strips16 * ((H + rpb16 - 1) / rpb16) < 2048) rpb16 = (rpb16 + 1) / 2;
+    hipLaunchKernelGGL(maxpool5_bwd_h16_kernel, dim3(strips16 * ((H + rpb16 - 1) / rpb16)), dim3(256), 0, st, SDP_H16(dp), idx,
+                       SDP_H16(res), SDP_H16W(dst), H, W, C, rpb16);
+  } else
     hipLaunchKernelGGL(maxpool5_bwd_kernel<float>, dim3(nb), dim3(256), 0, st, dp, reinterpret_cast<const uchar4*>(idx), res,
                        dst, H, W, C, rpb);
   return hipGetLastError();
