@@ -80,10 +80,9 @@ SDP_DEV float elu_grad(float t, int form) {
 // Arguments of one implicit-GEMM 3x3 / 1x1 convolution launch (activations NHWC float32).
 struct ConvArgs {
   const float* in;         // [B][H][W][Cin]
-  const uint4* wf;         // 32x32 fragment-ordered weights (train_aux.hip pack_slot): the exact-fp32
-                           //   forward "#frag" and every data gradient "#dfrag"
-  const uint4* wf16;       // forward weights in 16x16 fragment order "#frag16" (train_aux.hip
-                           //   pack_slot16): the bf16-mode forward
+  const uint4* wf;         // 32x32 fragment-ordered weights (train_aux.hip pack_slot): the exact-fp32 forward "#frag"
+  const uint4* wf16;       // weights in 16x16 fragment order (train_aux.hip pack_slot16): the bf16-mode forward
+                           //   "#frag16" and the data gradient "#dfrag16"
   const float* bias;       // [Cout] or null
   float* out;              // [B][Ho][Wo][Cout]  (Ho,Wo = H,W or H/2,W/2 when pooled)
   const float* res;        // residual, layout of out, or null

@@ -97,7 +97,9 @@ hipError_t conv_mfma(int mode, ConvArgs a, int ks, bool pool, hipStream_t st, co
   if (!a.pro_ss) { *why = "conv: prologue scale/shift table missing"; return hipErrorInvalidValue; }
   if (a.Cin > 1024 && a.ss_bstride == 0) { *why = "conv: identity table holds 1024 channels"; return hipErrorInvalidValue; }
   if (a.io16) {   // the bf16 training tape: the shapes the training plan launches (conv_launch.h IO16)
-#ifndef SDP_CONV_BENCH_ONLY
+#ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench io16: the 16-wide ELU-prologue tiles only
+    if (mode == MODE_BF16 && ks == 3 && tc == 16 && !pool) return conv_launch_nj2<MODE_BF16, true, 4, true>(a, st);
+#else
     if (mode != MODE_BF16) { *why = "conv: bf16 tensors (io16) need bf16 mode"; return hipErrorInvalidValue; }
     const bool pe = a.pro_mode != PRO_NONE;
     if (pool && ks == 1) return pe ? conv_launch<MODE_BF16, 1, 64, 1, true, true, true>(a, st)

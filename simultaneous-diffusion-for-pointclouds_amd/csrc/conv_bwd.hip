@@ -76,10 +76,12 @@ hipError_t conv_dgrad(int mode, ConvArgs a, int ks, hipStream_t st, const char**
   if (a.dact && !a.aux) { *why = "dgrad: dact needs aux"; return hipErrorInvalidValue; }
   if (a.dact == 3 && !a.epi_ss) { *why = "dgrad: dact 3 needs epi_ss"; return hipErrorInvalidValue; }
   if (!a.pro_ss) { *why = "dgrad: prologue identity table missing"; return hipErrorInvalidValue; }
-  if (!a.wf || a.wf16) { *why = "dgrad: weights in wf (the #dfrag packing), wf16 null"; return hipErrorInvalidValue; }
+  if (!a.wf16) { *why = "dgrad: weights in wf16 (the #dfrag16 packing)"; return hipErrorInvalidValue; }
   const bool t16 = ks == 3 && a.circular && Ws % 16 == 0 && Hs % 8 == 0;
   if (a.io16) {   // the bf16 training tape: the shapes the training plan launches (conv_launch.h IO16)
-#ifndef SDP_CONV_BENCH_ONLY
+#ifdef SDP_CONV_BENCH_ONLY   // tools/conv_bench io16: the 16-wide circular data gradients only
+    if (mode == MODE_BF16 && t16) return dgrad_launch_nj2<MODE_BF16, 4, true>(a, st);
+#else
     if (mode != MODE_BF16) { *why = "dgrad: bf16 tensors (io16) need bf16 mode"; return hipErrorInvalidValue; }
     if (ks == 1) return dgrad_launch<MODE_BF16, 2, 32, 1, false, true>(a, st);
     if (!a.circular) return dgrad_launch<MODE_BF16, 2, 32, 3, true, true>(a, st);

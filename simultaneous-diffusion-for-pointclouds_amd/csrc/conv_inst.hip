@@ -192,6 +192,8 @@ template hipError_t conv_launch_nj2<MODE_F32X3, true, 4>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_nj2<MODE_F32X3, true, 8>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_nj2<MODE_BF16, true, 4>(ConvArgs, hipStream_t);
 template hipError_t conv_launch_nj2<MODE_BF16, true, 8>(ConvArgs, hipStream_t);
+template hipError_t conv_launch_nj2<MODE_BF16, true, 4, true>(ConvArgs, hipStream_t);   // the bf16 tape (io16)
+template hipError_t dgrad_launch_nj2<MODE_BF16, 4, true>(ConvArgs, hipStream_t);
 #else
 #error "conv_inst.hip: build with -DSDP_INST=<code> (Makefile) or -DSDP_CONV_BENCH_ONLY (tools/conv_bench)"
 #endif

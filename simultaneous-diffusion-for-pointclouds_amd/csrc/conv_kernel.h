@@ -51,6 +51,10 @@ namespace sdp {
 #ifndef SDP_STORE_AUX
 #define SDP_STORE_AUX 2   // nt: the output streams to HBM without displacing the L2-resident weights
 #endif                    // (conv_bench 256->256 @32x512: 218 -> 214 us, tools/aux_run.sh)
+#ifndef SDP_STORE_AUX16   // the bf16-tape (IO16) epilogues: plain stores -- theirs are 32-B runs (16 bf16 channels of a
+#define SDP_STORE_AUX16 0  // pixel per instruction), which nt sends to HBM as partial lines; plain lets L2 merge them:
+#endif                     // bf16-tape training 183.7-184.3 -> 200.6-201.6 image-steps/s, 128->128 @64x1024 data
+                           // gradient 323 -> 285 us per B=8 launch (profiles/experiments/r06_store16_ab.log)
 
 #ifdef SDP_TIMING   // tools/conv_bench: per-workgroup phase clocks of wave 0 into a.dbg
 #define SDP_T(i) do { if (tid == 0) tclk[i] = __builtin_amdgcn_s_memtime(); } while (0)
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
   // weight fragments through a buffer resource: lane offset in a VGPR (fixed per nb), the
   // (chunk, tap) offset in an SGPR -> no per-load address arithmetic
   // SH 16 forward: the 16x16-native packing "#frag16" in wf16 (every fragment load of a wave reads
-  // 1 KiB contiguous); the data gradient (wf16 null, conv_dgrad checks it) reads the 32x32 "#dfrag"
+  // 1 KiB contiguous) -- the forward's "#frag16", the data gradient's "#dfrag16"; with wf16 null the 32x32 "#frag"
   // packing in wf in 16-B pieces per lane
   const bool c16 = SH == 16 && a.wf16 != nullptr;
   const __amdgpu_buffer_rsrc_t wrs =
@@ -965,7 +969,7 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
       if constexpr (!(SDP_KO & 16)) {
         static_for<0, 8>([&](auto mbc) {
           constexpr int mb = decltype(mbc)::value;
-          st(v[mb], ors, soff(mb, nj), std::integral_constant<int, SDP_STORE_AUX>{});
+          st(v[mb], ors, soff(mb, nj), std::integral_constant<int, IO16 ? SDP_STORE_AUX16 : SDP_STORE_AUX>{});
         });
       }
       if (a.stats) {
@@ -1163,7 +1167,8 @@ __global__ __launch_bounds__(64 * NW, NJ == 2 ? 2 : 1) void conv_mfma_kernel(Con
 #pragma unroll
         for (int i = 0; i < NV; ++i) v[i] = elu(v[i]);
       }
-      if constexpr (!(SDP_KO & 16)) store_vals(v, ors, njc, std::integral_constant<int, SDP_STORE_AUX>{});
+      if constexpr (!(SDP_KO & 16))
+        store_vals(v, ors, njc, std::integral_constant<int, IO16 ? SDP_STORE_AUX16 : SDP_STORE_AUX>{});
       if (a.stats) {
         float sum = 0.f;
 #pragma unroll

@@ -48,7 +48,7 @@ struct sdp_net {
   std::map<std::string, sdp::HostParam> host;
   // device tensors: parameters (pointers into `arena`), "sigmas", "#ident_ss" and the packed
   // conv weights "<key>#frag16" (forward, bf16 modes) or "<key>#frag" (forward, exact fp32) and
-  // "<key>#dfrag" (data gradient, training only)
+  // "<key>#dfrag16" (data gradient in 16x16 fragment order, training only)
   std::map<std::string, void*> dev;
   std::vector<sdp::ParamEntry> layout;
   float* arena = nullptr;           // every learnable parameter, fp32, `layout` order
@@ -127,15 +127,17 @@ struct sdp_net {
     for (auto& kv : host) {
       if (!is_conv_w(kv.first)) continue;
       const auto& s = kv.second.shape;
-      // packings: 0 = forward "#frag" (32x32 fragment order: the exact-fp32 forward), 1 = data
-      // gradient "#dfrag" (training), 3 = the forward in 16x16 fragment order "#frag16" (bf16 modes);
-      // (2 was the Winograd packing, removed with its kernel)
-      for (int dg = 0; dg < 4; ++dg) {
+      // packings: 0 = forward "#frag" (32x32 fragment order: the exact-fp32 forward), 3 = the forward in
+      // 16x16 fragment order "#frag16" (bf16 modes), 4 = the data gradient in 16x16 fragment order
+      // "#dfrag16" (training: bf16 modes); (1 was the data gradient in 32x32 order -- read in 16-B pieces
+      // at a 64-B lane stride, and in bf16 mode only the hi half of each 32 B: replaced in round 6 --
+      // 2 the Winograd packing, removed with its kernel)
+      for (int dg = 0; dg < 5; ++dg) {
         if (dg == 0 && mode != sdp::MODE_F32) continue;
-        if (dg == 1 && !train_packs) continue;
-        if (dg == 2) continue;
+        if (dg == 1 || dg == 2) continue;
         if (dg == 3 && mode == sdp::MODE_F32) continue;
-        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 1 ? "#dfrag" : "#frag16");
+        if (dg == 4 && (!train_packs || mode == sdp::MODE_F32)) continue;
+        const std::string fk = kv.first + (dg == 0 ? "#frag" : dg == 3 ? "#frag16" : "#dfrag16");
         const int nt = (int)(s[2] * s[3]);
         const size_t n = (size_t)s[0] * s[1] * nt;
         if (!dev.count(fk)) {

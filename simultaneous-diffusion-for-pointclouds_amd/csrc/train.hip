@@ -368,7 +368,7 @@ struct TrainPlan {
     if (dry) return;
     ConvArgs a{};
     a.in = dy.p;
-    a.wf = reinterpret_cast<const uint4*>(P(k + ".weight#dfrag"));
+    a.wf16 = reinterpret_cast<const uint4*>(P(k + ".weight#dfrag16"));   // coalesced 16x16 order (train_aux.hip pack_slot16)
     a.out = dx.p;
     a.res = res;
     a.pro_ss = P("#ident_ss");

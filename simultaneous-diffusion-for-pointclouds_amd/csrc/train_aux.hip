@@ -56,11 +56,13 @@ SDP_DEV uint32_t pack_slot(const float* __restrict__ w, int Cout, int Cin, int N
   return pk;
 }
 
-// 16x16 fragment order of the forward (conv_mfma_kernel SH = 16): [chunk][tap][nf = Cout/16][hl][lane 64]
-// [4 words = 8 bf16]; lane l: Cout nf*16 + l%16, channels chunk*32 + 8 (l/16) + 0..7 (hl: hi / lo part),
-// so every fragment load of a wave reads 1 KiB contiguous
-SDP_DEV uint32_t pack_slot16(const float* __restrict__ w, int Cout, int Cin, int NT, int mode, size_t i) {
-  const int NF = Cout / 16;
+// 16x16 fragment order of the bf16 modes (conv_mfma_kernel SH = 16): [chunk][tap][nf = Cout'/16][hl][lane 64]
+// [4 words = 8 bf16]; lane l: Cout' nf*16 + l%16, channels chunk*32 + 8 (l/16) + 0..7 (hl: hi / lo part),
+// so every fragment load of a wave reads 1 KiB contiguous (bf16 mode reads the hi blocks only).  dgrad:
+// the data gradient's flipped + transposed weights W'[o][i][tap] = W[i][o][k*k-1-tap] (Cout' = Cin) --
+// the same lane layout serves as the MFMA's A operand (the transposed D = W x X data gradient)
+SDP_DEV uint32_t pack_slot16(const float* __restrict__ w, int Cout, int Cin, int NT, int mode, int dgrad, size_t i) {
+  const int NF = (dgrad ? Cin : Cout) / 16;
   const int word = i & 3;
   const int lane = (i >> 2) & 63;
   const int hl = (i >> 8) & 1;
@@ -73,7 +75,7 @@ SDP_DEV uint32_t pack_slot16(const float* __restrict__ w, int Cout, int Cin, int
   uint32_t pk = 0;
   for (int e = 0; e < 2; ++e) {
     const int ci = ch * 32 + 8 * (lane >> 4) + word * 2 + e;
-    const float f = w[((size_t)co * Cin + ci) * NT + tap];
+    const float f = dgrad ? w[((size_t)ci * Cin + co) * NT + (NT - 1 - tap)] : w[((size_t)co * Cin + ci) * NT + tap];
     const __bf16 hi = (__bf16)f;
     const __bf16 q = (hl && mode == MODE_F32X3) ? (__bf16)(f - (float)hi) : hi;
     pk |= (uint32_t)__builtin_bit_cast(uint16_t, q) << (16 * e);
@@ -94,7 +96,7 @@ __global__ void pack_weights_multi_kernel(const PackDesc* __restrict__ d, int mo
   const PackDesc e = d[blockIdx.y];
   const size_t n = (size_t)e.Cout * e.Cin * e.NT;
   for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x)
-    e.out[j] = e.dgrad == 3 ? pack_slot16(e.w, e.Cout, e.Cin, e.NT, mode, j)
+    e.out[j] = e.dgrad >= 3 ? pack_slot16(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad == 4, j)
                             : pack_slot(e.w, e.Cout, e.Cin, e.NT, mode, e.dgrad, j);
 }
 

@@ -1,7 +1,8 @@
 // Standalone timing of one conv_mfma launch shape (diagnostics; links a conv.o built with
 // -DSDP_CONV_BENCH_ONLY [-DSDP_KO=mask]).  Usage: conv_bench Cin Cout H W B [dil] [iters] [mode]
 // (mode: 0 fp32, 1 fp32x3 (default), 2 bf16) [dgrad]: with a 9th argument "dgrad", the data gradient
-// (conv_dgrad: no prologue, epilogue * elu'(IN++ input, dact 3) + residual, as the training backward)
+// (conv_dgrad: no prologue, epilogue * elu'(IN++ input, dact 3) + residual, as the training backward);
+// a 10th argument "io16": the bf16-tape instantiation (bf16 tensors, mode 2 only; random bits serve)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -71,9 +72,10 @@ int main(int argc, char** argv) {
     std::vector<float> e2((size_t)B * Cout * 2);
     for (size_t i = 0; i < e2.size(); i += 2) { e2[i] = 1.f; e2[i + 1] = 0.f; }
     CK(hipMemcpy(ess, e2.data(), e2.size() * 4, hipMemcpyHostToDevice));
-    a.wf16 = nullptr; a.pro_mode = sdp::PRO_NONE; a.stats = nullptr; a.bias = nullptr;
+    a.pro_mode = sdp::PRO_NONE; a.stats = nullptr; a.bias = nullptr;   // (wf16: the #dfrag16 layout; random words serve)
     a.dact = 3; a.aux = aux; a.epi_ss = ess; a.res = res;
   }
+  if (argc > 10 && !strcmp(argv[10], "io16")) a.io16 = 1;   // (the fp32 buffers hold twice the bf16 elements needed)
   auto launch = [&]() { return dg ? sdp::conv_dgrad(mode, a, 3, 0, &why) : sdp::conv_mfma(mode, a, 3, false, 0, &why); };
   for (int i = 0; i < 3; ++i) CK(launch());
   CK(hipDeviceSynchronize());
