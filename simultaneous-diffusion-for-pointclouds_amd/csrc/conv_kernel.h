@@ -48,13 +48,15 @@ namespace sdp {
 #ifndef SDP_DMA_AUX
 #define SDP_DMA_AUX 0
 #endif
-#ifndef SDP_STORE_AUX
-#define SDP_STORE_AUX 2   // nt: the output streams to HBM without displacing the L2-resident weights
-#endif                    // (conv_bench 256->256 @32x512: 218 -> 214 us, tools/aux_run.sh)
-#ifndef SDP_STORE_AUX16   // the bf16-tape (IO16) epilogues: plain stores -- theirs are 32-B runs (16 bf16 channels of a
-#define SDP_STORE_AUX16 0  // pixel per instruction), which nt sends to HBM as partial lines; plain lets L2 merge them:
-#endif                     // bf16-tape training 183.7-184.3 -> 200.6-201.6 image-steps/s, 128->128 @64x1024 data
-                           // gradient 323 -> 285 us per B=8 launch (profiles/experiments/r06_store16_ab.log)
+#ifndef SDP_STORE_AUX     // plain (write-back) stores: each epilogue store instruction writes 64-B runs (fp32) or 32-B
+#define SDP_STORE_AUX 0   // runs (bf16 tape) of a pixel's channels, which L2 merges into whole lines before they leave
+#endif                    // for HBM; nt (2) sent them as partial lines.  Round 6 A/Bs (one box each, interleaved):
+                          // fp32x3 line 348.9-349.3 -> 361.8-363.1 image-steps/s (profiles/experiments/
+                          // r06_store_policy_ab.log); bf16-tape training 183.7-184.3 -> 200.6-201.6 (r06_store16_ab.log).
+                          // (Round 2 had measured no difference on the kernel of that time, 172.4 vs 172.6 us.)
+#ifndef SDP_STORE_AUX16   // the bf16-tape (IO16) epilogues
+#define SDP_STORE_AUX16 SDP_STORE_AUX
+#endif
 
 #ifdef SDP_TIMING   // tools/conv_bench: per-workgroup phase clocks of wave 0 into a.dbg
 #define SDP_T(i) do { if (tid == 0) tclk[i] = __builtin_amdgcn_s_memtime(); } while (0)
