@@ -26,7 +26,7 @@ sys.path.insert(0, os.path.join(REPO, "simultaneous-diffusion-for-pointclouds_am
 # label, kernel-name substring, threads per view along x (grid x), grid y (Cout / 128), FLOP per view,
 # MFMA passes, conv_bench C.  Both classes run conv_launch_nj2's 4-wave 128-Cout workgroups (NJ = 2):
 # the 256-Cout layers as two per tile (grid y = 2)
-NJ2 = "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false, 2>"
+NJ2 = "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false, 2, false>"   # (..., NJ, IO16)
 CLASSES = [
     ("conv3x3 256->256 @32x512 d1", NJ2, 256 * 256, 1, 2 * 256 * 256 * 9 * 32 * 512, 3, 256),
     ("conv3x3 128->128 @64x1024 d1", NJ2, 512 * 256, 1, 2 * 128 * 128 * 9 * 64 * 1024, 3, 128),
