@@ -184,7 +184,10 @@ __global__ __launch_bounds__(256, BC_WG_PER_CU) void begin_conv_kernel(const flo
 // the weight fragments are built once per workgroup, the next tile's image values are loaded into
 // registers (unconditional, clamped loads) while the current tile computes.  The FMA work of the
 // direct kernel (4608 per pixel on packed-f32 VALU) is what kept it off the HBM roofline.
-constexpr int BM_WG_PER_CU = 2, BM_TS = 68;   // workgroups per CU; transpose row stride (floats)
+#ifndef SDP_BM_WG         // workgroups per CU of the MFMA begin conv
+#define SDP_BM_WG 2
+#endif
+constexpr int BM_WG_PER_CU = SDP_BM_WG, BM_TS = 68;   // workgroups per CU; transpose row stride (floats)
 #ifndef SDP_BC_LDS_T      // 1: output stores through an LDS transpose (256-B runs); 0: straight from the C fragments
 #define SDP_BC_LDS_T 1
 #endif

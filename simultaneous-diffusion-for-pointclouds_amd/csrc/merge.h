@@ -31,6 +31,7 @@ struct MergeArgs {
   uint32_t* tcount;        // [T][nchunk], scanned in place
   uint32_t* bsum;          // scan block totals -> their exclusive scan (+ the grand total at [nb])
   uint32_t* toff;          // [T + 1] first record of every tile (+ the total): the segment passes' table
+  uint32_t* pstart;        // [T + 1] first part of every tile (+ the part count): the tile passes' table
   float4* rec;             // [pairs]: (code as 2 floats' bits, intensity, s << 10 | column)
   int32_t* pcell;          // [pairs]: K1's projection of every pair (big-grid cell or -1) and its
   double* pcode;           //   depth code, so K3 scatters without projecting again (same bits)

@@ -28,8 +28,22 @@ namespace sdp {
 // (KITTISampling.py:101-102, float64), the output views' grids reset (counts and sums 0, nearest code
 // and index all-ones) and the snapshot of the sources' intensities that the fused resolve+apply pass
 // reads while it corrects x in place.
+// The cos/sin of the W column azimuths and H row elevations are the same for every source view: each
+// workgroup computes them once into LDS (the grid is capped at MERGE_WORLD_WG workgroups, so a 32-view
+// megabatch evaluates 1/4 of the per-pixel sincos it did) -- the same float64 calls on the same arguments.
+constexpr int MERGE_WORLD_WG = 1024, MERGE_MAXH = 256;
 __global__ __launch_bounds__(256) void merge_world_kernel(MergeArgs a) {
+  __shared__ double2 tcz[1024], tce[MERGE_MAXH];   // (cos, sin) of column azimuths / row elevations
   const int H = a.g.H, W = a.g.W, HW = H * W;
+  for (int c = threadIdx.x; c < W; c += 256) {
+    const double az = (double)(W - 1 - c) * a.g.hA + a.g.hMin;
+    tcz[c] = make_double2(cos(az), sin(az));
+  }
+  for (int r = threadIdx.x; r < H; r += 256) {
+    const double el = (double)(H - 1 - r) * a.g.vA + a.g.vMin;
+    tce[r] = make_double2(cos(el), sin(el));
+  }
+  __syncthreads();
   const size_t n = (size_t)a.n_src * HW;
   const size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
   const size_t ncell = (size_t)a.n_out * a.g.big * W;
@@ -49,10 +63,8 @@ __global__ __launch_bounds__(256) void merge_world_kernel(MergeArgs a) {
     const float e = __fdiv_rn(__fmul_rn(fabsf(x0), 6.0f), a.smod);
     float rd = __fsub_rn(exp2f(e), 1.0f);
     if (x0 < 0.f) rd = -rd;
-    const double az = (double)(W - 1 - c) * a.g.hA + a.g.hMin;
-    const double el = (double)(H - 1 - r) * a.g.vA + a.g.vMin;
-    const double cz = cos(az), sz = sin(az);
-    const double ce = cos(el), se = sin(el);
+    const double cz = tcz[c].x, sz = tcz[c].y;
+    const double ce = tce[r].x, se = tce[r].y;
     const double rdd = (double)rd;
     double px = __dmul_rn(__dmul_rn(rdd, cz), ce);
     double py = __dmul_rn(__dmul_rn(rdd, sz), ce);
@@ -144,6 +156,22 @@ Proj project(const MergeArgs& a, double4 w, int o) {
 //                   contiguous lanes; a second sweep finds the lowest source index among the
 //                   nearest.  (One workgroup per tile was 5.9 ms: the horizon rows hold most
 //                   records.)
+// Tile passes (SDP_MERGE_TILE, the default): the records of one destination tile (output view, big row) are
+// summed by workgroups that each own a part of at most MERGE_TSEG of that tile's records and nothing else;
+// a tile of one part (most tiles) also finds its nearest indices and writes its row of cells with plain
+// stores -- no global atomics.  0 = the segment passes (4096 records per workgroup across tile boundaries).
+#ifndef SDP_MERGE_TILE
+#define SDP_MERGE_TILE 1
+#endif
+#ifndef SDP_MERGE_TSEG      // records per part
+#define SDP_MERGE_TSEG 2048
+#endif
+#ifndef SDP_MERGE_TNT       // threads per tile-pass workgroup
+#define SDP_MERGE_TNT 256
+#endif
+constexpr uint32_t MERGE_TSEG = SDP_MERGE_TSEG;
+constexpr int MERGE_TNT = SDP_MERGE_TNT;
+
 __device__ __forceinline__ void pair_of(const MergeArgs& a, size_t i, int HW, int& ol, int& s, int& o, int& m0) {
   const size_t per_out = (size_t)a.aB * HW;
   ol = (int)(i / per_out);
@@ -227,6 +255,33 @@ __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, siz
   if (blockIdx.x == 0) {   // chunk 0's cursors are the tiles' first records
     for (int t = tid; t < T; t += 256) a.toff[t] = cur[t];
     if (tid == 0) a.toff[T] = sb[nb];
+#if SDP_MERGE_TILE
+    // the tile passes' part table: tile t is cut into max(1, ceil(n_t / MERGE_TSEG)) parts of consecutive
+    // records; pstart = their exclusive scan (+ the part count at [T])
+    __shared__ uint32_t ps[256];
+    const int per = (T + 255) / 256, t0 = tid * per;
+    auto parts = [&](int t) {
+      const uint32_t n = (t + 1 < T ? cur[t + 1] : sb[nb]) - cur[t];
+      return n == 0u ? 1u : (n + MERGE_TSEG - 1) / MERGE_TSEG;
+    };
+    uint32_t loc = 0;
+    for (int k = 0; k < per; ++k) loc += t0 + k < T ? parts(t0 + k) : 0u;
+    ps[tid] = loc;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      const uint32_t y = tid >= off ? ps[tid - off] : 0u;
+      __syncthreads();
+      ps[tid] += y;
+      __syncthreads();
+    }
+    uint32_t run = ps[tid] - loc;
+    for (int k = 0; k < per; ++k)
+      if (t0 + k < T) {
+        a.pstart[t0 + k] = run;
+        run += parts(t0 + k);
+      }
+    if (tid == 255) a.pstart[T] = ps[255];
+#endif
   }
   __syncthreads();
   const size_t n = (size_t)a.n_out * a.aB * HW;
@@ -384,6 +439,183 @@ __global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a) {
   }
 }
 
+// K4 (tile passes): workgroup = part k of tile t (pstart table, written by merge_bin_scatter_kernel).  The
+// 1024 threads sum the part's records per cell in LDS (count, two float64 sums, nearest code).  A tile of one
+// part then sweeps its records again for the lowest source index among the nearest and stores its whole row
+// of cells (the grid reset of merge_world_kernel is overwritten); a part of a larger tile adds its touched
+// cells to the grids with atomics, and merge_tile_minidx_kernel finds those tiles' nearest indices.
+__device__ __forceinline__ int part_tile(const uint32_t* sps, uint32_t p, int T) {   // largest t: sps[t] <= p
+  int lo = 0, hi = T - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (sps[mid] <= p) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+__device__ __forceinline__ void rec_fields(const float4 r, unsigned long long& cb, uint32_t& w) {
+  cb = (unsigned long long)__float_as_uint(r.x) | ((unsigned long long)__float_as_uint(r.y) << 32);
+  w = __float_as_uint(r.w);
+}
+// Each thread takes a contiguous run of the part's records (not lane-interleaved ones): consecutive records are
+// consecutive source pixels, which mostly land in the same cell (in the 32-view bench megabatch 64 consecutive
+// records of the largest tile hit one cell 23 times on average), so the thread sums a run of equal cells in
+// registers and issues the LDS atomics once per run -- lane-interleaved records made those atomics collide.
+// With few sources per megabatch (the 4-view line) the collisions are rarer and lane-interleaved (coalesced)
+// records measured faster: RUNS = false walks the part with a stride of the workgroup (every record then
+// closes its own run).  Merge at 4 views 80 vs 93 us, at a 32-view megabatch 300 vs 343 us for runs
+// (profiles/experiments/r06_merge_tile_ab.log); the launcher picks RUNS for aB >= 16 sources.
+template <bool RUNS, typename F>
+__device__ __forceinline__ void for_runs(const MergeArgs& a, uint32_t r0, uint32_t r1, F&& f) {
+  constexpr int U = 4;                              // records in flight per thread
+  if constexpr (RUNS) {
+    const uint32_t per = (r1 - r0 + MERGE_TNT - 1) / MERGE_TNT;
+    const uint32_t b0 = r0 + threadIdx.x * per, b1 = min(r1, b0 + per);
+    for (uint32_t j = b0; j < b1; j += U) {
+      float4 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u] = a.rec[min(j + u, b1 - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j + u < b1) f(r[u]);
+    }
+  } else {
+    for (uint32_t j = r0 + threadIdx.x; j < r1; j += MERGE_TNT * U) {
+      float4 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u] = a.rec[min(j + MERGE_TNT * u, r1 - 1)];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j + MERGE_TNT * u < r1) f(r[u]);
+    }
+  }
+}
+template <bool RUNS>
+__global__ __launch_bounds__(MERGE_TNT) void merge_tile_sum_kernel(MergeArgs a) {
+  __shared__ uint32_t scnt[1024], sidx[1024];
+  __shared__ double ssl[1024], ssi[1024];
+  __shared__ unsigned long long smk[1024];
+  extern __shared__ uint32_t sps[];
+  const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big;
+  if (blockIdx.x >= a.pstart[T]) return;           // the grid is an upper bound of the part count
+  for (int t = tid; t <= T; t += MERGE_TNT) sps[t] = a.pstart[t];
+  for (int c = tid; c < W; c += MERGE_TNT) {
+    scnt[c] = 0u;
+    ssl[c] = 0.0;
+    ssi[c] = 0.0;
+    smk[c] = ~0ull;
+    sidx[c] = ~0u;
+  }
+  __syncthreads();
+  const int t = part_tile(sps, blockIdx.x, T);
+  const uint32_t k = blockIdx.x - sps[t], np = sps[t + 1] - sps[t];
+  const uint32_t tb = a.toff[t], te = a.toff[t + 1];
+  const uint32_t r0 = tb + k * MERGE_TSEG, r1 = min(te, r0 + MERGE_TSEG);
+  {
+    int rc = -1;                                    // the run's cell and its partial sums
+    uint32_t rn = 0u;
+    double rl = 0.0, ri = 0.0;
+    unsigned long long rm = ~0ull;
+    auto flush = [&]() {
+      if (rc < 0) return;
+      atomicAdd(&scnt[rc], rn);
+      atomicAdd(&ssl[rc], rl);
+      atomicAdd(&ssi[rc], ri);
+      atomicMin(&smk[rc], rm);
+    };
+    for_runs<RUNS>(a, r0, r1, [&](const float4 r) {
+      unsigned long long cb;
+      uint32_t w;
+      rec_fields(r, cb, w);
+      const int col = w & 1023u;
+      if (col != rc) {
+        flush();
+        rc = col;
+        rn = 0u;
+        rl = 0.0;
+        ri = 0.0;
+        rm = ~0ull;
+      }
+      ++rn;
+      rl += __longlong_as_double((long long)cb);
+      ri += (double)r.z;
+      rm = cb < rm ? cb : rm;
+    });
+    flush();
+  }
+  __syncthreads();
+  const size_t cb0 = (size_t)t * W;                 // tile t = ol * big + row -> cells row-major per view
+  if (np == 1u) {
+    int rc = -1;
+    uint32_t rs = ~0u;
+    for_runs<RUNS>(a, r0, r1, [&](const float4 r) {
+      unsigned long long cb;
+      uint32_t w;
+      rec_fields(r, cb, w);
+      const int col = w & 1023u;
+      if (col != rc) {
+        if (rc >= 0 && rs != ~0u) atomicMin(&sidx[rc], rs);
+        rc = col;
+        rs = ~0u;
+      }
+      if (cb == smk[col]) rs = min(rs, w >> 10);
+    });
+    if (rc >= 0 && rs != ~0u) atomicMin(&sidx[rc], rs);
+    __syncthreads();
+    for (int c = tid; c < W; c += MERGE_TNT) {
+      a.cnt[cb0 + c] = scnt[c];
+      a.sumL[cb0 + c] = ssl[c];
+      a.sumI[cb0 + c] = ssi[c];
+      a.minkey[cb0 + c] = smk[c];
+      a.minidx[cb0 + c] = sidx[c];
+    }
+    return;
+  }
+  for (int c = tid; c < W; c += MERGE_TNT) {
+    if (scnt[c] == 0u) continue;
+    atomicAdd(&a.cnt[cb0 + c], scnt[c]);
+    atomicAdd(&a.sumL[cb0 + c], ssl[c]);
+    atomicAdd(&a.sumI[cb0 + c], ssi[c]);
+    atomicMin(&a.minkey[cb0 + c], smk[c]);
+  }
+}
+// the nearest indices of the tiles of more than one part (the others were resolved by merge_tile_sum_kernel)
+template <bool RUNS>
+__global__ __launch_bounds__(MERGE_TNT) void merge_tile_minidx_kernel(MergeArgs a) {
+  __shared__ uint32_t sidx[1024];
+  extern __shared__ uint32_t sps[];
+  const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big;
+  if (blockIdx.x >= a.pstart[T]) return;
+  for (int t = tid; t <= T; t += MERGE_TNT) sps[t] = a.pstart[t];
+  for (int c = tid; c < W; c += MERGE_TNT) sidx[c] = ~0u;
+  __syncthreads();
+  const int t = part_tile(sps, blockIdx.x, T);
+  const uint32_t k = blockIdx.x - sps[t], np = sps[t + 1] - sps[t];
+  if (np == 1u) return;
+  const uint32_t r0 = a.toff[t] + k * MERGE_TSEG, r1 = min(a.toff[t + 1], r0 + MERGE_TSEG);
+  const size_t cb0 = (size_t)t * W;
+  int rc = -1;
+  uint32_t rs = ~0u;
+  unsigned long long mk = 0ull;
+  for_runs<RUNS>(a, r0, r1, [&](const float4 r) {
+    unsigned long long cb;
+    uint32_t w;
+    rec_fields(r, cb, w);
+    const int col = w & 1023u;
+    if (col != rc) {
+      if (rc >= 0 && rs != ~0u) atomicMin(&sidx[rc], rs);
+      rc = col;
+      rs = ~0u;
+      mk = a.minkey[cb0 + col];                     // one gather per run
+    }
+    if (cb == mk) rs = min(rs, w >> 10);
+  });
+  if (rc >= 0 && rs != ~0u) atomicMin(&sidx[rc], rs);
+  __syncthreads();
+  for (int c = tid; c < W; c += MERGE_TNT)
+    if (sidx[c] != ~0u) atomicMin(&a.minidx[cb0 + c], sidx[c]);
+}
+
 // ---------------------------------------------------------------- K5: resolve cells -> new image, apply
 // One pass per output pixel (the resolve and the correction were two launches): the cell the pixel
 // reads (flip/roll for negative depth), the controlled average (KITTISampling.py:300-420), the new
@@ -483,6 +715,7 @@ size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   add((size_t)n_out * 2 * H * W * 4);                        // newimg (internal)
   add((size_t)n_src * H * W * 4);                            // isnap
   add((T + 1) * 4);                                          // toff
+  add((T + 1) * 4);                                          // pstart
   return b + 1024;
 }
 
@@ -493,6 +726,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   if (ws_bytes < merge_ws_bytes(a.n_src, a.aB, a.n_out, H, W)) { *why = "merge: workspace too small"; return hipErrorInvalidValue; }
   if (a.n_src % a.aB || a.o_begin < 0 || a.o_begin + a.n_out > a.n_src) { *why = "merge: bad view ranges"; return hipErrorInvalidValue; }
   if (W % 2 || W > 1024) { *why = "merge: W must be even and <= 1024"; return hipErrorInvalidValue; }
+  if (H > MERGE_MAXH) { *why = "merge: H must be <= 256"; return hipErrorInvalidValue; }
   if ((size_t)a.aB * H * W > (1u << 22)) { *why = "merge: aB*H*W must be < 2^22 (record packing)"; return hipErrorInvalidValue; }
   const size_t npair = (size_t)a.n_out * a.aB * H * W, nout = (size_t)a.n_out * H * W, nw = (size_t)a.n_src * H * W;
   const int T = a.n_out * a.g.big;
@@ -516,6 +750,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   a.newimg = new_out ? new_out : reinterpret_cast<float*>(take((size_t)a.n_out * 2 * H * W * 4));
   a.isnap = reinterpret_cast<float*>(take(nw * 4));
   a.toff = reinterpret_cast<uint32_t*>(take(((size_t)T + 1) * 4));
+  a.pstart = reinterpret_cast<uint32_t*>(take(((size_t)T + 1) * 4));
   const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
   // dynamic LDS of each launch, checked against the per-workgroup limit BEFORE anything is enqueued:
   // count = the tile histogram [T]; scatter = the tile cursors [T] + the scanned block totals [nb + 1]
@@ -526,7 +761,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   constexpr size_t kDyn = 96 * 1024;   // the attribute set below (<= 160 KB per CU on gfx950)
   if (lds > kDyn) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
   if (slds + 1024 > kDyn) { *why = "merge: too many output views x chunks for the scatter's cursor + scan tables"; return hipErrorInvalidValue; }
-  if (tlds + 57 * 1024 > 152 * 1024) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
+  if (tlds + 57 * 1024 > 152 * 1024 || tlds + 33 * 1024 > kDyn) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
   hipError_t e;
   // the max-dynamic-LDS attribute acts on the current device: set once per device (thread-safe)
   {
@@ -537,7 +772,9 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
     std::lock_guard<std::mutex> lk(mu);
     if (dev >= 64 || !((done >> dev) & 1u)) {
       const void* fns[] = {(const void*)merge_bin_count_kernel, (const void*)merge_bin_scatter_kernel,
-                           (const void*)merge_seg_sum_kernel, (const void*)merge_seg_minidx_kernel};
+                           (const void*)merge_seg_sum_kernel, (const void*)merge_seg_minidx_kernel,
+                           (const void*)merge_tile_sum_kernel<false>, (const void*)merge_tile_minidx_kernel<false>,
+                           (const void*)merge_tile_sum_kernel<true>, (const void*)merge_tile_minidx_kernel<true>};
       for (const void* f : fns)
         if ((e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kDyn)) != hipSuccess) return e;
       if (dev < 64) done |= 1ull << dev;
@@ -545,13 +782,25 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   }
   // seven dependent launches: world (+ grid reset, intensity snapshot) -> count -> block scan ->
   // scatter (+ top scan, tile table) -> segment sums -> nearest index -> resolve + correction
-  hipLaunchKernelGGL(merge_world_kernel, dim3(grid_for(std::max(nw, (size_t)a.n_out * cells))), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(merge_world_kernel, dim3(std::min(grid_for(std::max(nw, (size_t)a.n_out * cells)), MERGE_WORLD_WG)),
+                     dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_bin_count_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
   hipLaunchKernelGGL(merge_scan_block_kernel, dim3(nb), dim3(256), 0, st, a.tcount, nt, a.bsum);
   hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), slds, st, a, per_chunk, nb);
+#if SDP_MERGE_TILE
+  const int nparts = (int)(T + (npair + MERGE_TSEG - 1) / MERGE_TSEG);   // upper bound: records <= pairs
+  if (a.aB >= 16) {
+    hipLaunchKernelGGL(merge_tile_sum_kernel<true>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
+    hipLaunchKernelGGL(merge_tile_minidx_kernel<true>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
+  } else {
+    hipLaunchKernelGGL(merge_tile_sum_kernel<false>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
+    hipLaunchKernelGGL(merge_tile_minidx_kernel<false>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
+  }
+#else
   const int nseg = (int)((npair + MERGE_SEG - 1) / MERGE_SEG);   // upper bound: records <= pairs
   hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), tlds, st, a);
   hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), tlds, st, a);
+#endif
   if (apply_wait && (e = hipStreamWaitEvent(st, apply_wait, 0)) != hipSuccess) return e;   // tooHigh's global max
   hipLaunchKernelGGL(merge_resolve_apply_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
   return hipGetLastError();

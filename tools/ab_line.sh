@@ -16,8 +16,9 @@ l = [x for x in open(sys.argv[3]) if x.startswith("{")][-1]
 d = json.loads(l)
 mb = {m["kernel"].split(" (")[0]: m["avg_launch_us"] for m in d["roofline"].get("memory_bound", [])}
 print(f"{sys.argv[1]:>12} r{sys.argv[2]}: {d['value']:8.2f} img-steps/s  {d['ms_per_step']:7.3f} ms  sustained "
-      f"{d.get('sustained', {}).get('value', 0):8.2f}  conv256 {d['roofline']['avg_launch_us']:.1f} us  merge "
+      f"{(d.get('sustained') or {}).get('value', 0):8.2f}  conv256 {d['roofline']['avg_launch_us']:.1f} us  merge "
       f"{mb.get('consistency_merge', 0):.1f} us", flush=True)
+print("      " + "  ".join(f"{k[:22]} {v:.1f}" for k, v in mb.items() if k != "consistency_merge"), flush=True)
 PY
   done
 done
