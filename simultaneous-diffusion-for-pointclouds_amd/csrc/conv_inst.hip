@@ -30,6 +30,12 @@ namespace sdp {
 #define SDP_CONV_CPAIR 1
 #endif
 
+// SDP_NJ2_STRIP (build-time A/B): strip tile order (conv_strip_w) for the 4-wave 32-Cout-wave launches too --
+// 1 = the paired 256-Cout layers, 2 = every 4-wave launch (the 128-channel layers as well)
+#ifndef SDP_NJ2_STRIP
+#define SDP_NJ2_STRIP 1
+#endif
+
 template <int MODE, int WM, int TC, int KS, bool POOL, bool PELU, bool IO16>
 hipError_t conv_launch(ConvArgs a, hipStream_t st) {
   using T = ConvTile<WM, TC, KS, 4, 4, IO16>;
@@ -68,10 +74,11 @@ hipError_t conv_launch_nj2(ConvArgs a, hipStream_t st) {
   using T = ConvTile<1, 16, 3, NW, 2, IO16>;
   a.tiles_per_img = a.H * a.W / (T::TR * 16);
   a.groups_per_img = a.H * a.W / 128;
-  a.strip_w = NW == 8 ? conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / 16) : 0;
   // two Cout blocks per tile (the fp32x3 256-Cout layers on 4-wave workgroups): dealt as adjacent pairs
   // of the XCD-ordered index, so a tile's second patch read comes from that XCD's L2
   a.cpair = (SDP_CONV_CPAIR && a.Cout == 2 * T::NTILE) ? 1 : 0;
+  const bool strip = NW == 8 || SDP_NJ2_STRIP == 2 || (SDP_NJ2_STRIP == 1 && a.cpair);
+  a.strip_w = strip ? conv_strip_w(a.H / a.dil / T::TR, a.W / a.dil / 16) : 0;
   dim3 grid(a.B * a.tiles_per_img * (a.cpair ? 2 : 1), a.cpair ? 1 : a.Cout / T::NTILE);
   hipLaunchKernelGGL((conv_mfma_kernel<MODE, 1, 16, 3, false, false, PELU, 16, NW, false, 2, IO16>), grid, dim3(T::NTH), 0,
                      st, a);

@@ -8,7 +8,7 @@ import sys
 
 from conftest import REPO
 
-NJ2 = "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false, 2>"
+NJ2 = "conv_mfma_kernel<1, 1, 16, 3, false, false, true, 16, 4, false, 2, false>"   # (..., NJ, IO16)
 CLASSES = [("256", 256 * 256, 2 * 256 * 256 * 9 * 32 * 512), ("128", 512 * 256, 2 * 128 * 128 * 9 * 64 * 1024)]
 
 

@@ -12,7 +12,18 @@ from oracle import scorenet_ref as R
 from oracle.gen_golden import CIRCLE_MODS, MERGE_CASES
 from sdp.weights import get_sigmas_np, synthetic_state_dict
 
-torch.set_num_threads(min(8, os.cpu_count() or 1))
+ORACLE_THREADS = min(8, os.cpu_count() or 1)
+
+
+@pytest.fixture(autouse=True)
+def _oracle_threads():
+    """The torch-CPU oracle's float32 convs round by their thread split: these checks (1e-6 of max) hold at the
+    thread count they were pinned with, whatever an earlier test of the session left set (an in-process
+    world-1 sampler run sets 1 thread)."""
+    prev = torch.get_num_threads()
+    torch.set_num_threads(ORACLE_THREADS)
+    yield
+    torch.set_num_threads(prev)
 
 
 def _g(name):
