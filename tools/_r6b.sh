@@ -1,0 +1,15 @@
+#!/bin/bash
+# round-6 session B: tile-aligned merge passes -- parity, per-kernel profile at 32 views, merge A/B
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/r6b; mkdir -p $O
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_config4.py tests/test_gpu_runner_pinned.py -x -q --timeout 200 --timeout-method thread > $O/parity.log 2>&1
+rc=$?; echo "parity rc=$rc"; tail -3 $O/parity.log; [ $rc -ne 0 ] && exit $rc
+for arm in tile0 tile1; do
+  if [ $arm = tile0 ]; then export SDP_LIB=tools/_var/tile0/libsdp.so; else unset SDP_LIB; fi
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/prof_$arm -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --megabatch-views 32 --no-cpu-baseline --no-fp32-line --split 1 --sustained-s 0 > $O/mb32_$arm.log 2>&1 || { echo "prof $arm failed"; tail -5 $O/mb32_$arm.log; exit 1; }
+  f=$(find $O/prof_$arm -name "run_kernel_stats.csv" | head -1); echo "== $arm"; python3 tools/stats_top.py $f 17 40 | grep -i "merge\|total"
+done
+unset SDP_LIB
+ARMS="tile0|SDP_LIB=tools/_var/tile0/libsdp.so|--megabatch-views 32;tile1||--megabatch-views 32;tile0_4|SDP_LIB=tools/_var/tile0/libsdp.so|;tile1_4||" bash tools/ab_line.sh
