@@ -151,18 +151,17 @@ Proj project(const MergeArgs& a, double4 w, int o) {
 //   scan          : exclusive offsets over [tile][chunk] (tile-major);
 //   K3 bin_scatter: the chunks read the kept projections back and write one 16-B record per pair
 //                   into their tile's range (LDS cursors);
-//   K4 segments   : workgroups take 4096 consecutive (so tile-sorted) records, sum them per
-//                   cell in LDS (ds atomics) and add each touched cell to the grids once, with
-//                   contiguous lanes; a second sweep finds the lowest source index among the
-//                   nearest.  (One workgroup per tile was 5.9 ms: the horizon rows hold most
-//                   records.)
-// Tile passes (SDP_MERGE_TILE, the default): the records of one destination tile (output view, big row) are
-// summed by workgroups that each own a part of at most MERGE_TSEG of that tile's records and nothing else;
-// a tile of one part (most tiles) also finds its nearest indices and writes its row of cells with plain
-// stores -- no global atomics.  0 = the segment passes (4096 records per workgroup across tile boundaries).
-#ifndef SDP_MERGE_TILE
-#define SDP_MERGE_TILE 1
-#endif
+//   K4 tile passes: workgroups take parts of <= MERGE_TSEG records of ONE tile, sum them per cell in
+//                   LDS (ds atomics) and store (one-part tile) or add once per touched cell (larger
+//                   tiles) to the grids; a second sweep finds the lowest source index among the
+//                   nearest.  (One workgroup per whole tile was 5.9 ms: the horizon rows hold most
+//                   records -- 8 % of a 32-view megabatch's records land in one row.)
+// Tile passes: the records of one destination tile (output view, big row) are summed by workgroups that each
+// own a part of at most MERGE_TSEG of that tile's records and nothing else; a tile of one part (most tiles)
+// also finds its nearest indices and writes its row of cells with plain stores -- no global atomics.  They
+// replace round 5's segment passes (4096 consecutive records per workgroup across tile boundaries, records of
+// a third tile onward straight to global atomics): 32-view megabatch merge 360-363 -> 301-305 us, 4 views
+// 113-115 -> 84-85 us (profiles/experiments/r06_merge_tile_ab.log).
 #ifndef SDP_MERGE_TSEG      // records per part
 #define SDP_MERGE_TSEG 2048
 #endif
@@ -215,7 +214,7 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
 
 // The top level of the offset scan rides here (one launch less): every workgroup scans the nb block
 // totals of merge_scan_block_kernel in LDS; workgroup 0 also publishes every tile's first record and
-// the total (toff) for the segment passes, which run after this launch.  The scan is redundant work:
+// the total (toff) and the part table (pstart) for the tile passes, which run after this launch.  The scan is redundant work:
 // each of the nchunk workgroups reads all nb totals from L2 (nchunk * nb loads, at most 1024 x 8192) --
 // cheaper than the launch it replaces at the measured sizes (4 views: 156 -> 110 us for the whole chain,
 // a 32-view config-4 rank 401 -> 352 us; profiles/experiments/r05_merge_chain_ab.log).
@@ -255,7 +254,6 @@ __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, siz
   if (blockIdx.x == 0) {   // chunk 0's cursors are the tiles' first records
     for (int t = tid; t < T; t += 256) a.toff[t] = cur[t];
     if (tid == 0) a.toff[T] = sb[nb];
-#if SDP_MERGE_TILE
     // the tile passes' part table: tile t is cut into max(1, ceil(n_t / MERGE_TSEG)) parts of consecutive
     // records; pstart = their exclusive scan (+ the part count at [T])
     __shared__ uint32_t ps[256];
@@ -281,7 +279,6 @@ __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, siz
         run += parts(t0 + k);
       }
     if (tid == 255) a.pstart[T] = ps[255];
-#endif
   }
   __syncthreads();
   const size_t n = (size_t)a.n_out * a.aB * HW;
@@ -331,112 +328,6 @@ __global__ __launch_bounds__(256) void merge_scan_block_kernel(uint32_t* __restr
     run += x[k];
   }
   if (tid == 255) bsum[blockIdx.x] = sh[255];
-}
-
-// the tile whose range holds record j (largest t with toff[t] <= j), on the LDS copy of the table
-__device__ __forceinline__ int tile_of(const uint32_t* toff, uint32_t j, int T) {
-  int lo = 0, hi = T - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (toff[mid] <= j) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-// the tile table [T + 1] into LDS (dynamic shared memory after the kernel's static arrays)
-__device__ __forceinline__ void load_toff(const MergeArgs& a, uint32_t* st, int T) {
-  for (int t = threadIdx.x; t <= T; t += 256) st[t] = a.toff[t];
-}
-
-// K4a: a workgroup sums MERGE_SEG consecutive records (tile-sorted) in LDS over the first two
-// tiles they touch (records of further tiles, a sparse stretch, go straight to global
-// atomics) and adds its cells to the grids: one atomic per touched cell, contiguous lanes.
-// The tile of a record comes from the tile table in LDS (one global binary search per record of a
-// sparse stretch before: a chain of dependent L2 loads).
-constexpr int MERGE_SEG = 4096;
-__global__ __launch_bounds__(256) void merge_seg_sum_kernel(MergeArgs a) {
-  __shared__ uint32_t scnt[2048];
-  __shared__ double ssl[2048], ssi[2048];
-  __shared__ unsigned long long smk[2048];
-  extern __shared__ uint32_t stoff[];
-  const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big, big = a.g.big;
-  load_toff(a, stoff, T);
-  for (int c = tid; c < 2 * W; c += 256) {
-    scnt[c] = 0u;
-    ssl[c] = 0.0;
-    ssi[c] = 0.0;
-    smk[c] = ~0ull;
-  }
-  __syncthreads();
-  const uint32_t total = stoff[T];
-  const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
-  if (j0 >= total) return;
-  const int t0 = tile_of(stoff, j0, T);
-  const uint32_t e1 = stoff[min(t0 + 1, T)], e2 = stoff[min(t0 + 2, T)];
-  for (uint32_t j = j0 + tid; j < j1; j += 256) {
-    const float4 r = a.rec[j];
-    const unsigned long long cb =
-        (unsigned long long)__float_as_uint(r.x) | ((unsigned long long)__float_as_uint(r.y) << 32);
-    const int col = __float_as_uint(r.w) & 1023u;
-    const double code = __longlong_as_double((long long)cb);
-    if (j < e2) {
-      const int c = (j < e1 ? 0 : W) + col;
-      atomicAdd(&scnt[c], 1u);
-      atomicAdd(&ssl[c], code);
-      atomicAdd(&ssi[c], (double)r.z);
-      atomicMin(&smk[c], cb);
-    } else {
-      const int t = tile_of(stoff, j, T);
-      const size_t ci = ((size_t)(t / big) * big + t % big) * W + col;
-      atomicAdd(&a.cnt[ci], 1u);
-      atomicAdd(&a.sumL[ci], code);
-      atomicAdd(&a.sumI[ci], (double)r.z);
-      atomicMin(&a.minkey[ci], cb);
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < 2 * W; c += 256) {
-    const int t = t0 + c / W;
-    if (t >= T || scnt[c] == 0u) continue;
-    const size_t ci = (size_t)t * W + c % W;     // tile t = ol * big + row -> cell row-major per view
-    atomicAdd(&a.cnt[ci], scnt[c]);
-    atomicAdd(&a.sumL[ci], ssl[c]);
-    atomicAdd(&a.sumI[ci], ssi[c]);
-    atomicMin(&a.minkey[ci], smk[c]);
-  }
-}
-
-// K4b: the lowest source index among the records whose code equals the cell's nearest code
-__global__ __launch_bounds__(256) void merge_seg_minidx_kernel(MergeArgs a) {
-  __shared__ uint32_t sidx[2048];
-  extern __shared__ uint32_t stoff[];
-  const int tid = threadIdx.x, W = a.g.W, T = a.n_out * a.g.big;
-  load_toff(a, stoff, T);
-  for (int c = tid; c < 2 * W; c += 256) sidx[c] = 0xffffffffu;
-  __syncthreads();
-  const uint32_t total = stoff[T];
-  const uint32_t j0 = blockIdx.x * MERGE_SEG, j1 = min(total, j0 + MERGE_SEG);
-  if (j0 >= total) return;
-  const int t0 = tile_of(stoff, j0, T);
-  const uint32_t e1 = stoff[min(t0 + 1, T)], e2 = stoff[min(t0 + 2, T)];
-  for (uint32_t j = j0 + tid; j < j1; j += 256) {
-    const float4 r = a.rec[j];
-    const unsigned long long cb =
-        (unsigned long long)__float_as_uint(r.x) | ((unsigned long long)__float_as_uint(r.y) << 32);
-    const uint32_t w = __float_as_uint(r.w);
-    const int col = w & 1023u;
-    const int t = j < e2 ? (j < e1 ? t0 : t0 + 1) : tile_of(stoff, j, T);
-    const size_t ci = (size_t)t * W + col;
-    if (cb != a.minkey[ci]) continue;
-    if (j < e2) atomicMin(&sidx[(j < e1 ? 0 : W) + col], w >> 10);
-    else atomicMin(&a.minidx[ci], w >> 10);
-  }
-  __syncthreads();
-  for (int c = tid; c < 2 * W; c += 256) {
-    const int t = t0 + c / W;
-    if (t >= T || sidx[c] == 0xffffffffu) continue;
-    atomicMin(&a.minidx[(size_t)t * W + c % W], sidx[c]);
-  }
 }
 
 // K4 (tile passes): workgroup = part k of tile t (pstart table, written by merge_bin_scatter_kernel).  The
@@ -754,14 +645,14 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
   // dynamic LDS of each launch, checked against the per-workgroup limit BEFORE anything is enqueued:
   // count = the tile histogram [T]; scatter = the tile cursors [T] + the scanned block totals [nb + 1]
-  // beside its 1 KB static scan array; segment passes = the tile table [T + 1] beside 57 KB static
+  // beside its 1 KB static scan array; tile passes = the part table [T + 1] beside 32 KB static
   const size_t lds = (size_t)T * 4;
   const size_t slds = lds + ((size_t)nb + 1) * 4;
   const size_t tlds = ((size_t)T + 1) * 4;
   constexpr size_t kDyn = 96 * 1024;   // the attribute set below (<= 160 KB per CU on gfx950)
   if (lds > kDyn) { *why = "merge: too many output views for the tile histogram"; return hipErrorInvalidValue; }
   if (slds + 1024 > kDyn) { *why = "merge: too many output views x chunks for the scatter's cursor + scan tables"; return hipErrorInvalidValue; }
-  if (tlds + 57 * 1024 > 152 * 1024 || tlds + 33 * 1024 > kDyn) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
+  if (tlds + 33 * 1024 > kDyn) { *why = "merge: too many output views for the tile table"; return hipErrorInvalidValue; }
   hipError_t e;
   // the max-dynamic-LDS attribute acts on the current device: set once per device (thread-safe)
   {
@@ -772,7 +663,6 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
     std::lock_guard<std::mutex> lk(mu);
     if (dev >= 64 || !((done >> dev) & 1u)) {
       const void* fns[] = {(const void*)merge_bin_count_kernel, (const void*)merge_bin_scatter_kernel,
-                           (const void*)merge_seg_sum_kernel, (const void*)merge_seg_minidx_kernel,
                            (const void*)merge_tile_sum_kernel<false>, (const void*)merge_tile_minidx_kernel<false>,
                            (const void*)merge_tile_sum_kernel<true>, (const void*)merge_tile_minidx_kernel<true>};
       for (const void* f : fns)
@@ -781,13 +671,13 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
     }
   }
   // seven dependent launches: world (+ grid reset, intensity snapshot) -> count -> block scan ->
-  // scatter (+ top scan, tile table) -> segment sums -> nearest index -> resolve + correction
+  // scatter (+ top scan, tile and part tables) -> tile sums (+ the nearest index of one-part tiles) ->
+  // nearest index of the other tiles -> resolve + correction
   hipLaunchKernelGGL(merge_world_kernel, dim3(std::min(grid_for(std::max(nw, (size_t)a.n_out * cells)), MERGE_WORLD_WG)),
                      dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_bin_count_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
   hipLaunchKernelGGL(merge_scan_block_kernel, dim3(nb), dim3(256), 0, st, a.tcount, nt, a.bsum);
   hipLaunchKernelGGL(merge_bin_scatter_kernel, dim3(a.nchunk), dim3(256), slds, st, a, per_chunk, nb);
-#if SDP_MERGE_TILE
   const int nparts = (int)(T + (npair + MERGE_TSEG - 1) / MERGE_TSEG);   // upper bound: records <= pairs
   if (a.aB >= 16) {
     hipLaunchKernelGGL(merge_tile_sum_kernel<true>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
@@ -796,11 +686,6 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
     hipLaunchKernelGGL(merge_tile_sum_kernel<false>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
     hipLaunchKernelGGL(merge_tile_minidx_kernel<false>, dim3(nparts), dim3(MERGE_TNT), tlds, st, a);
   }
-#else
-  const int nseg = (int)((npair + MERGE_SEG - 1) / MERGE_SEG);   // upper bound: records <= pairs
-  hipLaunchKernelGGL(merge_seg_sum_kernel, dim3(nseg), dim3(256), tlds, st, a);
-  hipLaunchKernelGGL(merge_seg_minidx_kernel, dim3(nseg), dim3(256), tlds, st, a);
-#endif
   if (apply_wait && (e = hipStreamWaitEvent(st, apply_wait, 0)) != hipSuccess) return e;   // tooHigh's global max
   hipLaunchKernelGGL(merge_resolve_apply_kernel, dim3(grid_for(nout)), dim3(256), 0, st, a);
   return hipGetLastError();
