@@ -33,5 +33,9 @@ fi
 if [ "$PART" = 3 ] || [ "$PART" = all ]; then
 step rocprof 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fp32-line --split 1 --sustained-s 0
 step rocprof_train 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run --output-format csv -- python bench.py --workload train --steps 5 --warmup 1 --no-cpu-baseline
+step rocprof_mb32 300 rocprofv3 --kernel-trace --stats -d $O/prof_mb32 -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --megabatch-views 32 --no-cpu-baseline --no-fp32-line --split 1 --sustained-s 0
+# the default two-stream step (--split 2): how much of each memory-bound kernel runs under a conv of the other stream
+step rocprof_split2 300 rocprofv3 --kernel-trace -d $O/prof_split2 -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-fp32-line --sustained-s 0
+step overlap 120 python3 tools/overlap.py $(find $O/prof_split2 -name "run_kernel_trace.csv" | head -1) $O/${ROUND:-r05}_overlap.json
 fi
 exit 0
