@@ -132,7 +132,9 @@ Proj project(const MergeArgs& a, double4 w, int o) {
   const double fr = rint(__ddiv_rn(__dsub_rn(e, a.g.bigMin), a.g.vA));
   const int col = a.g.W - 1 - (int)fc;
   const int row = a.g.big - 1 - (int)fr;
-  bool ok = w.w != 0.0 && col > -1 && col < a.g.W && row > -1 && row < a.g.big;
+  // a NaN bin (a NaN or infinite world point) fails the reference's range test (numpy comparisons with NaN
+  // are false); (int) of NaN is 0 here, so it is excluded explicitly
+  bool ok = w.w != 0.0 && fc == fc && fr == fr && col > -1 && col < a.g.W && row > -1 && row < a.g.big;
   // setting 5 (kitti) / always (AllForOne): min-depth filter code > log2(1.2)/6*smod
   if (a.variant == 1 || a.setting == 5) ok = ok && code > (double)a.min_code;
   if (ok) pr.cell = row * a.g.W + col;
@@ -565,13 +567,17 @@ __global__ __launch_bounds__(256) void merge_resolve_apply_kernel(MergeArgs a) {
     const bool m = nn > 0 && a.exist[p] && a.sky[(size_t)o * HW + p];
     a.newimg[((size_t)ol * 2 + 0) * HW + p] = depth;
     a.newimg[((size_t)ol * 2 + 1) * HW + p] = inten;
-    if (too_high || !m) continue;
-    // KITTISampling.py:470-490: x += cc * -(x - new) where the reference mask is 0
-    if (a.refmask[x0i] == 0) a.xout[x0i] = __fadd_rn(xd, __fmul_rn(a.cc, -__fsub_rn(xd, depth)));
-    if (a.refmask[x0i + HW] == 0) {
-      const float xi = a.xout[x0i + HW];
-      a.xout[x0i + HW] = __fadd_rn(xi, __fmul_rn(a.cc, -__fsub_rn(xi, inten)));
-    }
+    if (too_high) continue;
+    // KITTISampling.py:428-490: x += cc * -(maskImages * !mask * (x - new)).  Where the factor is 0 the
+    // product is still NaN when x - new is not finite (a NaN intensity in the cell, an infinite x), and the
+    // reference's x becomes NaN there; elsewhere it leaves x as it is.
+    const float d0 = __fsub_rn(xd, depth);
+    if (m && a.refmask[x0i] == 0) a.xout[x0i] = __fadd_rn(xd, __fmul_rn(a.cc, -d0));
+    else if (!isfinite(d0)) a.xout[x0i] = __int_as_float(0x7fc00000);
+    const float xi = a.xout[x0i + HW];
+    const float d1 = __fsub_rn(xi, inten);
+    if (m && a.refmask[x0i + HW] == 0) a.xout[x0i + HW] = __fadd_rn(xi, __fmul_rn(a.cc, -d1));
+    else if (!isfinite(d1)) a.xout[x0i + HW] = __int_as_float(0x7fc00000);
   }
 }
 

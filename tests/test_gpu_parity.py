@@ -283,6 +283,43 @@ def test_kitti_merge_matches_reference_golden(case_def):
     _assert_merge_exact(new, f["new"], _final_dc(xc, case), f["x"], fl, tag)
 
 
+def test_kitti_merge_nan_points_match_oracle():
+    """NaN codes and intensities in the merged views (a NaN x[:, 0] reaches the merge as a NaN world point; the
+    Langevin golden carries NaN/inf lanes): the reference's numpy projection gives NaN bins, which fail its
+    range test, so such a point lands nowhere (KITTISampling.py:244-251), while a NaN intensity poisons the
+    sums of the cell it lands in.  The device must not turn a NaN bin into a cell index (a float64 -> int
+    conversion of NaN is 0 on gfx950), and the NaN pattern of the outputs must be the oracle's."""
+    import warnings
+    from sdp.merge import Merger
+    tag, B, aB, H, W, sigma, kw = MERGE_CASES[0]
+    case = GI.merge_case(tag, B, H, W, **kw)
+    x = _after_update(case)
+    r = np.random.default_rng(5)
+    idx = r.choice(H * W, 40, replace=False)
+    x.reshape(B, 2, -1)[:, 0, idx[:20]] = np.nan
+    x.reshape(B, 2, -1)[:, 1, idx[20:]] = np.nan
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        want_new, want_x, fl = S.kitti_merge(x, case["mask"], case["sky"], case["exist"], case["toWorld"],
+                                             case["fromWorld"], aB, sigma, flags=True)
+    xg = torch.from_numpy(x).to(DEV)
+    m = Merger(B, aB, H, W, DEV, torch.from_numpy(case["exist"]), torch.from_numpy(case["sky"]),
+               torch.from_numpy(case["mask"]), toWorld=torch.from_numpy(case["toWorld"]),
+               fromWorld=torch.from_numpy(case["fromWorld"]))
+    absmax = torch.tensor([np.nan], dtype=torch.float32).view(torch.int32).to(DEV)   # max|x| of the oracle: NaN
+    new = torch.empty(B, 2, H, W, device=DEV)
+    m(xg, sigma, 5, 10, 0.01, absmax, new)
+    got_new, got_x = new.cpu().numpy(), xg.cpu().numpy()
+    ok = ~np.broadcast_to(fl[:, None], got_new.shape)
+    assert np.isnan(want_new).any() and np.isnan(want_x).any()
+    assert np.array_equal(np.isnan(got_new) & ok, np.isnan(want_new) & ok)
+    assert np.array_equal(np.isnan(got_x) & ok, np.isnan(want_x) & ok)
+    fin = ok & ~np.isnan(want_new)
+    assert np.all(np.abs(got_new - want_new)[fin] <= 2e-6 + 1e-5 * np.abs(want_new)[fin])
+    finx = ok & ~np.isnan(want_x)
+    assert np.all(np.abs(got_x - want_x)[finx] <= 2e-6 + 1e-5 * np.abs(want_x)[finx])
+
+
 @pytest.mark.parametrize("tag,setting", [("a_b7_s05_set7", 7), ("a_b7_s05_set5", 5), ("a_b7_s05_set8", 8)])
 def test_allforone_merge_matches_reference_golden(tag, setting):
     """Settings 5 (cc ramp), 7 (controlled average) and 8 (controlled, allowance 5:
