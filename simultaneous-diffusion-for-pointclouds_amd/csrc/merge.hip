@@ -99,9 +99,6 @@ struct Proj {
 #ifndef SDP_MERGE_INLINE
 #define SDP_MERGE_INLINE 1
 #endif
-#ifndef SDP_MERGE_UNROLL   // pairs per thread and iteration of the count pass (world loads issued together)
-#define SDP_MERGE_UNROLL 1
-#endif
 #if SDP_MERGE_INLINE
 __device__ __forceinline__
 #else
@@ -147,7 +144,8 @@ Proj project(const MergeArgs& a, double4 w, int o) {
 // scattered addresses), and every pair needs four (count, two sums, nearest code): a 32-view
 // megabatch spent 3.8 ms of an 18.8-ms step there.  Instead the pairs are binned by
 // destination tile = (output view, big-grid row):
-//   K1 bin_count  : each chunk of pairs projects its points, counts them per tile (LDS) and keeps
+//   K1 bin_count  : each chunk (a range of source points x every output view) projects its points,
+//                   counts them per tile (LDS) and keeps
 //                   every pair's (cell, code) -- the float64 projection (two atan2, log2, sqrt)
 //                   is the costly part of both binning passes;
 //   scan          : exclusive offsets over [tile][chunk] (tile-major);
@@ -173,40 +171,33 @@ Proj project(const MergeArgs& a, double4 w, int o) {
 constexpr uint32_t MERGE_TSEG = SDP_MERGE_TSEG;
 constexpr int MERGE_TNT = SDP_MERGE_TNT;
 
-__device__ __forceinline__ void pair_of(const MergeArgs& a, size_t i, int HW, int& ol, int& s, int& o, int& m0) {
-  const size_t per_out = (size_t)a.aB * HW;
-  ol = (int)(i / per_out);
-  s = (int)(i % per_out);
-  o = a.o_begin + ol;
-  m0 = (o / a.aB) * a.aB;
-}
-
 __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_t per_chunk) {
   extern __shared__ uint32_t hist[];
   const int HW = a.g.H * a.g.W, T = a.n_out * a.g.big;
   for (int t = threadIdx.x; t < T; t += 256) hist[t] = 0u;
   __syncthreads();
-  const size_t n = (size_t)a.n_out * a.aB * HW;
-  const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
-  constexpr int U = SDP_MERGE_UNROLL;
-  for (size_t i = i0 + threadIdx.x; i < i1; i += 256 * U) {
-    int ol[U], s[U], o[U], m0[U];
-    double4 wv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {   // clamped pair index: every load unconditional
-      const size_t ii = min(i + 256 * u, i1 - 1);
-      pair_of(a, ii, HW, ol[u], s[u], o[u], m0[u]);
-      wv[u] = a.world[(size_t)m0[u] * HW + s[u]];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const size_t ii = i + 256 * u;
-      if (ii >= i1) break;
-      const Proj pr = project(a, wv[u], o[u]);
+  // chunk = a range of source points, each projected into every output view in turn (the view loop is
+  // wave-uniform, so the view's pose is a scalar load): a source's world point is read once, not once per
+  // output view (a config-4 rank: 67 instead of 268 MB).  Count 126 -> 111 us and merge 289-291 -> 277-279
+  // us at a 32-view megabatch, bit-identical (profiles/experiments/r06_merge_srcmajor_ab.log); round 5's
+  // source-major numbering had put a different view in every lane (per-lane pose gathers) and was slower.
+  const size_t per_out = (size_t)a.aB * HW;
+  const size_t s0 = blockIdx.x * per_chunk, s1 = s0 + per_chunk < per_out ? s0 + per_chunk : per_out;
+  for (size_t sp = s0 + threadIdx.x; sp < s1; sp += 256) {
+    int m0p = -1;
+    double4 wv = make_double4(0.0, 0.0, 0.0, 0.0);
+    for (int ol = 0; ol < a.n_out; ++ol) {
+      const int o = a.o_begin + ol, m0 = (o / a.aB) * a.aB;
+      if (m0 != m0p) {
+        wv = a.world[(size_t)m0 * HW + sp];
+        m0p = m0;
+      }
+      const Proj pr = project(a, wv, o);
+      const size_t ii = (size_t)ol * per_out + sp;
       a.pcell[ii] = pr.cell;
       if (pr.cell >= 0) {
         a.pcode[ii] = pr.code;
-        atomicAdd(&hist[ol[u] * a.g.big + pr.cell / a.g.W], 1u);
+        atomicAdd(&hist[ol * a.g.big + pr.cell / a.g.W], 1u);
       }
     }
   }
@@ -283,13 +274,13 @@ __global__ __launch_bounds__(256) void merge_bin_scatter_kernel(MergeArgs a, siz
     if (tid == 255) a.pstart[T] = ps[255];
   }
   __syncthreads();
-  const size_t n = (size_t)a.n_out * a.aB * HW;
-  const size_t i0 = blockIdx.x * per_chunk, i1 = i0 + per_chunk < n ? i0 + per_chunk : n;
-  for (size_t i = i0 + tid; i < i1; i += 256) {
+  const size_t per_out = (size_t)a.aB * HW;
+  const size_t s0 = blockIdx.x * per_chunk, s1 = s0 + per_chunk < per_out ? s0 + per_chunk : per_out;
+  for (int olc = 0; olc < a.n_out; ++olc)           // view by view: consecutive lanes, consecutive pairs
+  for (size_t i = (size_t)olc * per_out + s0 + tid; i < (size_t)olc * per_out + s1; i += 256) {
     const int cell = a.pcell[i];
     if (cell < 0) continue;
-    int ol, s, o, m0;
-    pair_of(a, i, HW, ol, s, o, m0);
+    const int ol = olc, s = (int)(i - (size_t)olc * per_out), o = a.o_begin + ol, m0 = (o / a.aB) * a.aB;
     Proj pr;
     pr.cell = cell;
     pr.code = a.pcode[i];
@@ -648,7 +639,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   a.isnap = reinterpret_cast<float*>(take(nw * 4));
   a.toff = reinterpret_cast<uint32_t*>(take(((size_t)T + 1) * 4));
   a.pstart = reinterpret_cast<uint32_t*>(take(((size_t)T + 1) * 4));
-  const size_t per_chunk = (npair + a.nchunk - 1) / a.nchunk;
+  const size_t per_chunk = ((size_t)a.aB * H * W + a.nchunk - 1) / a.nchunk;   // source points per chunk
   // dynamic LDS of each launch, checked against the per-workgroup limit BEFORE anything is enqueued:
   // count = the tile histogram [T]; scatter = the tile cursors [T] + the scanned block totals [nb + 1]
   // beside its 1 KB static scan array; tile passes = the part table [T + 1] beside 32 KB static
