@@ -17,7 +17,7 @@ struct MergeArgs {
   const uint8_t* exist;    // [aB][HW]
   const uint8_t* sky;      // [n_src][HW]
   const int32_t* refmask;  // [n_src][2][HW]
-  double4* world;          // [n_src][HW] world point + source-valid flag
+  double2* trig;           // [W + H] (cos, sin) of the column azimuths, then of the row elevations
   float* isnap;            // [n_src][HW] the sources' intensity channel before the correction (resolve's
                            //   nearest-point intensity reads it while the fused pass corrects x in place)
   // per-cell results [n_out][cells] (cells = big x W), written once per cell by merge_tile

@@ -23,29 +23,25 @@
 
 namespace sdp {
 
-// ---------------------------------------------------------------- K0: source points -> world
-// Also (one launch instead of four): the cos/sin of the point's column azimuth and row elevation
-// (KITTISampling.py:101-102, float64), the output views' grids reset (counts and sums 0, nearest code
-// and index all-ones) and the snapshot of the sources' intensities that the fused resolve+apply pass
-// reads while it corrects x in place.
-// The cos/sin of the W column azimuths and H row elevations are the same for every source view: each
-// workgroup computes them once into LDS (the grid is capped at MERGE_WORLD_WG workgroups, so a 32-view
-// megabatch evaluates 1/4 of the per-pixel sincos it did) -- the same float64 calls on the same arguments.
-constexpr int MERGE_WORLD_WG = 1024, MERGE_MAXH = 256;
-__global__ __launch_bounds__(256) void merge_world_kernel(MergeArgs a) {
-  __shared__ double2 tcz[1024], tce[MERGE_MAXH];   // (cos, sin) of column azimuths / row elevations
+// ---------------------------------------------------------------- K0: prep
+// One launch: the output views' grids reset (counts and sums 0, nearest code and index all-ones), the
+// snapshot of the sources' intensities that the fused resolve+apply pass reads while it corrects x in place,
+// and the (cos, sin) table of the W column azimuths and H row elevations (KITTISampling.py:101-102,
+// float64) that the count pass's world points use.  (Until round 6 this kernel also wrote every source's
+// float64 world point, 32 B each, which the count pass read back: the count pass now computes them itself,
+// once per source point -- profiles/experiments/r06_merge_fused_world_ab.log.)
+constexpr int MERGE_PREP_WG = 1024;
+__global__ __launch_bounds__(256) void merge_prep_kernel(MergeArgs a) {
   const int H = a.g.H, W = a.g.W, HW = H * W;
-  for (int c = threadIdx.x; c < W; c += 256) {
-    const double az = (double)(W - 1 - c) * a.g.hA + a.g.hMin;
-    tcz[c] = make_double2(cos(az), sin(az));
-  }
-  for (int r = threadIdx.x; r < H; r += 256) {
-    const double el = (double)(H - 1 - r) * a.g.vA + a.g.vMin;
-    tce[r] = make_double2(cos(el), sin(el));
-  }
-  __syncthreads();
   const size_t n = (size_t)a.n_src * HW;
   const size_t i0 = blockIdx.x * (size_t)blockDim.x + threadIdx.x, stride = (size_t)gridDim.x * blockDim.x;
+  if (i0 < (size_t)W) {
+    const double az = (double)(W - 1 - (int)i0) * a.g.hA + a.g.hMin;
+    a.trig[i0] = make_double2(cos(az), sin(az));
+  } else if (i0 < (size_t)(W + H)) {
+    const double el = (double)(H - 1 - (int)(i0 - W)) * a.g.vA + a.g.vMin;
+    a.trig[i0] = make_double2(cos(el), sin(el));
+  }
   const size_t ncell = (size_t)a.n_out * a.g.big * W;
   for (size_t c = i0; c < ncell; c += stride) {
     a.cnt[c] = 0u;
@@ -56,36 +52,41 @@ __global__ __launch_bounds__(256) void merge_world_kernel(MergeArgs a) {
   }
   for (size_t i = i0; i < n; i += stride) {
     const int v = i / HW, p = i % HW;
-    const int r = p / W, c = p % W;
-    const float x0 = a.x[(size_t)v * 2 * HW + p];
     a.isnap[i] = a.x[(size_t)v * 2 * HW + HW + p];
-    // realDistance = (2^(|x|*6/smod) - 1) * (+-1), float32 (KITTISampling.py:164-166)
-    const float e = __fdiv_rn(__fmul_rn(fabsf(x0), 6.0f), a.smod);
-    float rd = __fsub_rn(exp2f(e), 1.0f);
-    if (x0 < 0.f) rd = -rd;
-    const double cz = tcz[c].x, sz = tcz[c].y;
-    const double ce = tce[r].x, se = tce[r].y;
-    const double rdd = (double)rd;
-    double px = __dmul_rn(__dmul_rn(rdd, cz), ce);
-    double py = __dmul_rn(__dmul_rn(rdd, sz), ce);
-    double pz = __dmul_rn(rdd, se);
-    const int vl = v % a.aB;
-    double flag = a.exist[(size_t)vl * HW + p] ? 1.0 : 0.0;
-    double4 w;
-    if (a.variant == 0) {
-      const double* T = a.toWorld + (size_t)v * 16;
-      w.x = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(T[0], px), __dmul_rn(T[1], py)), __dmul_rn(T[2], pz)), T[3]);
-      w.y = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(T[4], px), __dmul_rn(T[5], py)), __dmul_rn(T[6], pz)), T[7]);
-      w.z = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(T[8], px), __dmul_rn(T[9], py)), __dmul_rn(T[10], pz)), T[11]);
-    } else {
-      w.x = __dadd_rn(px, (double)a.origins[vl * 3 + 0]);
-      w.y = __dadd_rn(py, (double)a.origins[vl * 3 + 1]);
-      w.z = __dadd_rn(pz, (double)a.origins[vl * 3 + 2]);
-      if (!a.sky[(size_t)v * HW + p]) flag = 0.0;   // source sky gate (models/__init__.py:356-359)
-    }
-    w.w = flag;
-    a.world[i] = w;
   }
+}
+
+// world point of source view v, pixel p (+ the source-valid flag in .w), from the prep kernel's trig table
+__device__ __forceinline__ double4 world_point(const MergeArgs& a, int v, int p) {
+  const int HW = a.g.H * a.g.W, W = a.g.W;
+  const int r = p / W, c = p - r * W;
+  const float x0 = a.x[(size_t)v * 2 * HW + p];
+  // realDistance = (2^(|x|*6/smod) - 1) * (+-1), float32 (KITTISampling.py:164-166)
+  const float e = __fdiv_rn(__fmul_rn(fabsf(x0), 6.0f), a.smod);
+  float rd = __fsub_rn(exp2f(e), 1.0f);
+  if (x0 < 0.f) rd = -rd;
+  const double2 tz = a.trig[c], te = a.trig[W + r];
+  const double cz = tz.x, sz = tz.y, ce = te.x, se = te.y;
+  const double rdd = (double)rd;
+  double px = __dmul_rn(__dmul_rn(rdd, cz), ce);
+  double py = __dmul_rn(__dmul_rn(rdd, sz), ce);
+  double pz = __dmul_rn(rdd, se);
+  const int vl = v % a.aB;
+  double flag = a.exist[(size_t)vl * HW + p] ? 1.0 : 0.0;
+  double4 w;
+  if (a.variant == 0) {
+    const double* T = a.toWorld + (size_t)v * 16;
+    w.x = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(T[0], px), __dmul_rn(T[1], py)), __dmul_rn(T[2], pz)), T[3]);
+    w.y = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(T[4], px), __dmul_rn(T[5], py)), __dmul_rn(T[6], pz)), T[7]);
+    w.z = __dadd_rn(__dadd_rn(__dadd_rn(__dmul_rn(T[8], px), __dmul_rn(T[9], py)), __dmul_rn(T[10], pz)), T[11]);
+  } else {
+    w.x = __dadd_rn(px, (double)a.origins[vl * 3 + 0]);
+    w.y = __dadd_rn(py, (double)a.origins[vl * 3 + 1]);
+    w.z = __dadd_rn(pz, (double)a.origins[vl * 3 + 2]);
+    if (!a.sky[(size_t)v * HW + p]) flag = 0.0;   // source sky gate (models/__init__.py:356-359)
+  }
+  w.w = flag;
+  return w;
 }
 
 struct Proj {
@@ -177,8 +178,9 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
   for (int t = threadIdx.x; t < T; t += 256) hist[t] = 0u;
   __syncthreads();
   // chunk = a range of source points, each projected into every output view in turn (the view loop is
-  // wave-uniform, so the view's pose is a scalar load): a source's world point is read once, not once per
-  // output view (a config-4 rank: 67 instead of 268 MB).  Count 126 -> 111 us and merge 289-291 -> 277-279
+  // wave-uniform, so the view's pose is a scalar load): a source's world point is computed once (since
+  // the fused prep: from x and the trig table; before, read from a 32-B world array) and projected into
+  // every view, not read once per output view (a config-4 rank read 268 MB of world points).  Count 126 -> 111 us and merge 289-291 -> 277-279
   // us at a 32-view megabatch, bit-identical (profiles/experiments/r06_merge_srcmajor_ab.log); round 5's
   // source-major numbering had put a different view in every lane (per-lane pose gathers) and was slower.
   const size_t per_out = (size_t)a.aB * HW;
@@ -189,7 +191,8 @@ __global__ __launch_bounds__(256) void merge_bin_count_kernel(MergeArgs a, size_
     for (int ol = 0; ol < a.n_out; ++ol) {
       const int o = a.o_begin + ol, m0 = (o / a.aB) * a.aB;
       if (m0 != m0p) {
-        wv = a.world[(size_t)m0 * HW + sp];
+        const uint32_t s32 = (uint32_t)sp;   // < aB * HW < 2^22 (checked by the launcher)
+        wv = world_point(a, m0 + (int)(s32 / (uint32_t)HW), (int)(s32 % (uint32_t)HW));
         m0p = m0;
       }
       const Proj pr = project(a, wv, o);
@@ -589,7 +592,7 @@ size_t merge_ws_bytes(int n_src, int aB, int n_out, int H, int W) {
   const size_t T = (size_t)n_out * big, nt = T * merge_chunks(npair);
   size_t b = 0;
   auto add = [&](size_t x) { b += (x + 255) & ~size_t(255); };
-  add((size_t)n_src * H * W * sizeof(double4));             // world
+  add((size_t)(W + H) * sizeof(double2));                    // trig
   add(cells * n_out * 4);                                    // cnt
   add(cells * n_out * 8);                                    // sumL
   add(cells * n_out * 8);                                    // sumI
@@ -614,8 +617,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   if (ws_bytes < merge_ws_bytes(a.n_src, a.aB, a.n_out, H, W)) { *why = "merge: workspace too small"; return hipErrorInvalidValue; }
   if (a.n_src % a.aB || a.o_begin < 0 || a.o_begin + a.n_out > a.n_src) { *why = "merge: bad view ranges"; return hipErrorInvalidValue; }
   if (W % 2 || W > 1024) { *why = "merge: W must be even and <= 1024"; return hipErrorInvalidValue; }
-  if (H > MERGE_MAXH) { *why = "merge: H must be <= 256"; return hipErrorInvalidValue; }
-  if ((size_t)a.aB * H * W > (1u << 22)) { *why = "merge: aB*H*W must be < 2^22 (record packing)"; return hipErrorInvalidValue; }
+    if ((size_t)a.aB * H * W > (1u << 22)) { *why = "merge: aB*H*W must be < 2^22 (record packing)"; return hipErrorInvalidValue; }
   const size_t npair = (size_t)a.n_out * a.aB * H * W, nout = (size_t)a.n_out * H * W, nw = (size_t)a.n_src * H * W;
   const int T = a.n_out * a.g.big;
   a.nchunk = merge_chunks(npair);
@@ -624,7 +626,7 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
   if (nb > 8 * 1024) { *why = "merge: too many tiles x chunks"; return hipErrorInvalidValue; }
   char* p = reinterpret_cast<char*>(ws);
   auto take = [&](size_t bytes) { char* q = p; p += (bytes + 255) & ~size_t(255); return q; };
-  a.world = reinterpret_cast<double4*>(take(nw * sizeof(double4)));
+  a.trig = reinterpret_cast<double2*>(take((size_t)(W + H) * sizeof(double2)));
   a.cnt = reinterpret_cast<uint32_t*>(take(cells * a.n_out * 4));
   a.sumL = reinterpret_cast<double*>(take(cells * a.n_out * 8));
   a.sumI = reinterpret_cast<double*>(take(cells * a.n_out * 8));
@@ -667,10 +669,10 @@ hipError_t consistency_merge(MergeArgs a, void* ws, size_t ws_bytes, float* new_
       if (dev < 64) done |= 1ull << dev;
     }
   }
-  // seven dependent launches: world (+ grid reset, intensity snapshot) -> count -> block scan ->
+  // seven dependent launches: prep (grid reset, intensity snapshot, trig table) -> count (+ world points) -> block scan ->
   // scatter (+ top scan, tile and part tables) -> tile sums (+ the nearest index of one-part tiles) ->
   // nearest index of the other tiles -> resolve + correction
-  hipLaunchKernelGGL(merge_world_kernel, dim3(std::min(grid_for(std::max(nw, (size_t)a.n_out * cells)), MERGE_WORLD_WG)),
+  hipLaunchKernelGGL(merge_prep_kernel, dim3(std::min(grid_for(std::max(nw, (size_t)a.n_out * cells)), MERGE_PREP_WG)),
                      dim3(256), 0, st, a);
   hipLaunchKernelGGL(merge_bin_count_kernel, dim3(a.nchunk), dim3(256), lds, st, a, per_chunk);
   hipLaunchKernelGGL(merge_scan_block_kernel, dim3(nb), dim3(256), 0, st, a.tcount, nt, a.bsum);
