@@ -51,6 +51,7 @@ hipError_t upsample_backward(const float* g, float* dlow, int B, int H, int W, i
 hipError_t elu_backward_post(const float* dy, const float* y, const float* res, float* dst, size_t n, hipStream_t st,
                              bool h16 = false);
 hipError_t add_tensors(const float* a, const float* b, float* dst, size_t n, hipStream_t st, bool h16 = false);
+size_t head_wgrad_part_floats(int B, int H, int W);   // scratch of begin_conv_wgrad / end_conv_backward
 hipError_t begin_conv_wgrad(const float* x, const float* dy, float* part, float* dw, float* db, int B, int H, int W,
                             hipStream_t st, bool h16 = false);
 hipError_t end_conv_backward(const float* dscore, const float* sigmas, const int64_t* labels, const float* w,

@@ -502,7 +502,7 @@ struct TrainPlan {
     coef = take((size_t)B * 256 * 4);
     bpart = take(1024 * 256);
     ppart = take((size_t)B * 256 * 3);
-    epart = take(std::max((size_t)B * (H / 32) * (W / 32) * (2 * 128 * 9 + 2), (size_t)B * (H / 32) * (W / 64) * 128 * 37));
+    epart = take(head_wgrad_part_floats(B, H, W));
     if (!dry) ok(hipMemsetAsync(grads, 0, net->arena_floats * 4, st), "zero grads");
 
     // head: IN++ -> ELU -> end_conv -> / sigma

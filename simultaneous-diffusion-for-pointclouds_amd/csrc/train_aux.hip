@@ -684,7 +684,9 @@ SDP_DEV float linspace01_t(int i, int n) {
   return i < n / 2 ? step * (float)i : 1.0f - step * (float)(n - 1 - i);
 }
 
-constexpr int BW_ROWS = 32;
+// 8 rows per block: B * H/8 * W/64 blocks (1024 at B=8, 64x1024) keep four waves per SIMD in flight; 32 rows gave
+// 256 blocks, one wave per SIMD, and every LDS read of the FMA loop stood exposed (387 us per call at B=8)
+constexpr int BW_ROWS = 8;
 template <typename TA>
 __global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restrict__ x, const TA* __restrict__ dy,
                                                           float* __restrict__ part, int H, int W) {
@@ -790,7 +792,9 @@ __global__ __launch_bounds__(256) void end_dgrad_kernel(const float* __restrict_
   }
 }
 
-constexpr int EW_ROWS = 32;
+// 16 rows per block (1024 blocks at B=8); the transformed input rows sit in a 3-slot ring, each row is
+// loaded and pushed through IN++ + ELU once (it was staged afresh for each of the 3 output rows that read it)
+constexpr int EW_ROWS = 16;
 template <typename TA>
 __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict__ dscore, const float* __restrict__ sigmas,
                                                         const int64_t* __restrict__ labels, const TA* __restrict__ o,
@@ -809,12 +813,12 @@ __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict_
 #pragma unroll
   for (int k = 0; k < 9; ++k) acc[k] = 0.f;
   float db = 0.f;
-  for (int r = 0; r < EW_ROWS; ++r) {
-    const int y = y0 + r;
-    __syncthreads();
-    for (int i = tid; i < 3 * 34 * 32; i += 256) {
-      const int pix = i >> 5, c4 = i & 31, rr = pix / 34, cc = pix % 34;
-      const int yy = y - 1 + rr, xx = x0 - 1 + cc;
+  // input row yy (y0 - 1 <= yy <= y0 + EW_ROWS) lives in ring slot (yy - y0 + 1) % 3
+  auto stage_row = [&](int yy) {
+    const int slot = (yy - y0 + 1) % 3;
+    for (int i = tid; i < 34 * 32; i += 256) {
+      const int cc = i >> 5, c4 = i & 31;
+      const int xx = x0 - 1 + cc;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
         const float4 h = ldg4(o, (((size_t)b * H + yy) * W + xx) * C + c4 * 4);
@@ -822,19 +826,30 @@ __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict_
         v = make_float4(elu(fmaf(h.x, s0.x, s0.y)), elu(fmaf(h.y, s0.z, s0.w)), elu(fmaf(h.z, s1.x, s1.y)),
                         elu(fmaf(h.w, s1.z, s1.w)));
       }
-      *reinterpret_cast<float4*>(&sp[pix * C + c4 * 4]) = v;
+      *reinterpret_cast<float4*>(&sp[(slot * 34 + cc) * C + c4 * 4]) = v;
     }
+  };
+  stage_row(y0 - 1);
+  stage_row(y0);
+  for (int r = 0; r < EW_ROWS; ++r) {
+    const int y = y0 + r;
+    stage_row(y + 1);                                // slot of row y - 2, read last by iteration r - 1
     if (tid < 64) {
       const int c2 = tid >> 5, px = tid & 31;
       sd[c2][px] = dscore[(((size_t)b * 2 + c2) * H + y) * W + x0 + px] * inv;
     }
     __syncthreads();
+    const int sl0 = r % 3, sl1 = (r + 1) % 3, sl2 = (r + 2) % 3;   // slots of rows y - 1, y, y + 1
     for (int px = 0; px < 32; ++px) {
       const float gv = sd[co][px];
       if (ci == 0) db += gv;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) acc[tap] = fmaf(gv, sp[((tap / 3) * 34 + px + tap % 3) * C + ci], acc[tap]);
+      for (int tap = 0; tap < 9; ++tap) {
+        const int sl = tap / 3 == 0 ? sl0 : (tap / 3 == 1 ? sl1 : sl2);
+        acc[tap] = fmaf(gv, sp[(sl * 34 + px + tap % 3) * C + ci], acc[tap]);
+      }
     }
+    __syncthreads();                                 // the ring slot and sd are rewritten next iteration
   }
   float* op = part + (size_t)blockIdx.x * (2 * C * 9 + 2);
 #pragma unroll
@@ -858,6 +873,13 @@ hipError_t end_conv_backward(const float* dscore, const float* sigmas, const int
   }
   (void)sum_rows(part, nb, 2 * 128 * 9, 2 * 128 * 9 + 2, dw, st);
   return sum_rows(part + 2 * 128 * 9, nb, 2, 2 * 128 * 9 + 2, db, st);
+}
+
+// floats of the partial-sum scratch the head weight gradients need (begin_conv_wgrad, end_conv_backward)
+size_t head_wgrad_part_floats(int B, int H, int W) {
+  const size_t bw = (size_t)B * (H / BW_ROWS) * (W / 64) * 128 * 37;
+  const size_t ew = (size_t)B * (H / EW_ROWS) * (W / 32) * (2 * 128 * 9 + 2);
+  return bw > ew ? bw : ew;
 }
 
 // ---------------------------------------------------------------- DSM loss (losses/dsm.py:67-119)
