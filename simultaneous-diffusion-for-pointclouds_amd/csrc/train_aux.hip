@@ -721,14 +721,36 @@ __global__ __launch_bounds__(256) void begin_wgrad_kernel(const float* __restric
       sd[px][c4 * 4] = v.x; sd[px][c4 * 4 + 1] = v.y; sd[px][c4 * 4 + 2] = v.z; sd[px][c4 * 4 + 3] = v.w;
     }
     __syncthreads();
+    // the thread's two input channels (2 half, 2 half + 1) x 3 rows x 3 columns in registers, one new column
+    // per pixel: 6 LDS reads per 18 FMAs instead of 18 (the same FMAs in the same order)
+    const int ci0 = half * 2;
+    float wv[2][3][3];
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+      for (int rr = 0; rr < 3; ++rr) {
+        wv[c2][rr][0] = sp[ci0 + c2][rr][0];
+        wv[c2][rr][1] = sp[ci0 + c2][rr][1];
+      }
     for (int px = 0; px < 64; ++px) {
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) wv[c2][rr][2] = sp[ci0 + c2][rr][px + 2];
       const float g = sd[px][co];
       if (half == 0) db += g;
 #pragma unroll
       for (int k = 0; k < 18; ++k) {
-        const int j = half * 18 + k, ci = j / 9, tap = j % 9;
-        acc[k] = fmaf(g, sp[ci][tap / 3][px + tap % 3], acc[k]);
+        const int c2 = k / 9, tap = k % 9;
+        acc[k] = fmaf(g, wv[c2][tap / 3][tap % 3], acc[k]);
       }
+#pragma unroll
+      for (int c2 = 0; c2 < 2; ++c2)
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+          wv[c2][rr][0] = wv[c2][rr][1];
+          wv[c2][rr][1] = wv[c2][rr][2];
+        }
     }
   }
   float* o = part + (size_t)blockIdx.x * (128 * 37);
@@ -839,14 +861,26 @@ __global__ __launch_bounds__(256) void end_wgrad_kernel(const float* __restrict_
       sd[c2][px] = dscore[(((size_t)b * 2 + c2) * H + y) * W + x0 + px] * inv;
     }
     __syncthreads();
-    const int sl0 = r % 3, sl1 = (r + 1) % 3, sl2 = (r + 2) % 3;   // slots of rows y - 1, y, y + 1
+    const int sl[3] = {r % 3, (r + 1) % 3, (r + 2) % 3};   // slots of rows y - 1, y, y + 1
+    // the thread's channel at 3 rows x 3 columns in registers, one new column per pixel (3 LDS reads per 9
+    // FMAs instead of 9; the same FMAs in the same order)
+    float wv[3][3];
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      wv[kh][0] = sp[(sl[kh] * 34 + 0) * C + ci];
+      wv[kh][1] = sp[(sl[kh] * 34 + 1) * C + ci];
+    }
     for (int px = 0; px < 32; ++px) {
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) wv[kh][2] = sp[(sl[kh] * 34 + px + 2) * C + ci];
       const float gv = sd[co][px];
       if (ci == 0) db += gv;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int sl = tap / 3 == 0 ? sl0 : (tap / 3 == 1 ? sl1 : sl2);
-        acc[tap] = fmaf(gv, sp[(sl * 34 + px + tap % 3) * C + ci], acc[tap]);
+      for (int tap = 0; tap < 9; ++tap) acc[tap] = fmaf(gv, wv[tap / 3][tap % 3], acc[tap]);
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        wv[kh][0] = wv[kh][1];
+        wv[kh][1] = wv[kh][2];
       }
     }
     __syncthreads();                                 // the ring slot and sd are rewritten next iteration
